@@ -1,0 +1,170 @@
+"""ctypes front-end for the CPU oracle (oracle/_build/libur3e_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and the
+bench.py `cpu_baseline` leg as the checker.  The product package (ur3e_amd)
+never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "_build", "libur3e_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB):
+        subprocess.run(["make", "-C", _HERE], check=True, stdout=subprocess.DEVNULL)
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB)
+    return _lib
+
+
+class OracleConfig(ctypes.Structure):
+    _fields_ = [
+        ("task", ctypes.c_int), ("frame_skip", ctypes.c_int), ("max_episode_steps", ctypes.c_int),
+        ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
+        ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
+        ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
+    ]
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class OracleBatch:
+    """N independent oracle envs with the same step semantics as ur3e_batch_step."""
+
+    def __init__(self, model_c, cfg: OracleConfig, n_envs: int):
+        self.L = lib()
+        self.m = model_c
+        self.cfg = cfg
+        self.n = n_envs
+        self.nq, self.nv = model_c.nq, model_c.nv
+        self.buf = ctypes.create_string_buffer(self.L.ur3o_sizeof_env() * n_envs)
+        self.obs = np.zeros((n_envs, 24))
+        self.L.ur3o_batch_init(ctypes.byref(self.m), ctypes.byref(self.cfg), ctypes.c_int(n_envs), self.buf,
+                               _p(self.obs))
+
+    def step(self, actions: np.ndarray):
+        actions = np.ascontiguousarray(actions, dtype=np.float64)
+        n = self.n
+        obs = np.zeros((n, 24))
+        rew = np.zeros(n)
+        term = np.zeros(n, np.uint8)
+        trunc = np.zeros(n, np.uint8)
+        tobs = np.zeros((n, 24))
+        self.L.ur3o_batch_step(ctypes.byref(self.m), ctypes.byref(self.cfg), ctypes.c_int(n), self.buf,
+                               _p(actions), ctypes.c_int(actions.shape[1]), _p(obs), _p(rew), _p(term),
+                               _p(trunc), _p(tobs))
+        self.obs = obs
+        return obs, rew, term, trunc, tobs
+
+    def get_state(self):
+        qp = np.zeros((self.n, self.nq))
+        qv = np.zeros((self.n, self.nv))
+        wa = np.zeros((self.n, self.nv))
+        nc = np.zeros(self.n, np.int32)
+        self.L.ur3o_batch_get_state(ctypes.byref(self.m), ctypes.c_int(self.n), self.buf, _p(qp), _p(qv), _p(wa),
+                                    _p(nc))
+        return qp, qv, wa, nc
+
+    def set_state(self, qpos, qvel, warm=None):
+        qpos = np.ascontiguousarray(qpos, dtype=np.float64)
+        qvel = np.ascontiguousarray(qvel, dtype=np.float64)
+        warm = None if warm is None else np.ascontiguousarray(warm, dtype=np.float64)
+        self.L.ur3o_batch_set_state(ctypes.byref(self.m), ctypes.c_int(self.n), self.buf, _p(qpos), _p(qvel),
+                                    _p(warm))
+
+    def diag(self, i):
+        ncon, nefc, nit = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        touch = np.zeros(4)
+        sz = self.L.ur3o_sizeof_env()
+        ptr = ctypes.cast(ctypes.addressof(self.buf) + sz * i, ctypes.c_void_p)
+        self.L.ur3o_env_diag(ptr, ctypes.byref(ncon), ctypes.byref(nefc), ctypes.byref(nit), _p(touch))
+        return dict(ncon=ncon.value, nefc=nefc.value, niter=nit.value, touch=touch)
+
+
+def forward_state(model_c, qpos, qvel=None):
+    L = lib()
+    nq, nv, ns = model_c.nq, model_c.nv, model_c.nsite
+    qpos = np.ascontiguousarray(qpos, dtype=np.float64)
+    qvel = np.zeros(nv) if qvel is None else np.ascontiguousarray(qvel, dtype=np.float64)
+    sx = np.zeros((max(ns, 1), 3))
+    sm = np.zeros((max(ns, 1), 9))
+    bias = np.zeros(nv)
+    M = np.zeros((nv, nv))
+    ncon = ctypes.c_int()
+    L.ur3o_forward_state(ctypes.byref(model_c), _p(qpos), _p(qvel), _p(sx), _p(sm), _p(bias), _p(M),
+                         ctypes.byref(ncon))
+    return dict(site_xpos=sx, site_xmat=sm, qfrc_bias=bias, qM=M, ncon=ncon.value)
+
+
+def rot_err(xmat, target):
+    L = lib()
+    xmat = np.ascontiguousarray(xmat, dtype=np.float64).reshape(9)
+    target = np.ascontiguousarray(target, dtype=np.float64)
+    out = np.zeros(3)
+    L.ur3o_rot_err(_p(xmat), _p(target), _p(out))
+    return out
+
+
+def pid_task_ctrl_raw(traj7, tcp_xpos, tcp_xmat, jac_arm, qvel6, bias6, gains12, grip_scale=255.0):
+    L = lib()
+
+    class TG(ctypes.Structure):
+        _fields_ = [("g", ctypes.c_double * 12)]
+
+    tg = TG()
+    for k in range(12):
+        tg.g[k] = gains12[k]
+    a = [np.ascontiguousarray(x, dtype=np.float64).reshape(-1) for x in (traj7, tcp_xpos, tcp_xmat, jac_arm, qvel6, bias6)]
+    out = np.zeros(7)
+    L.ur3o_pid_task_ctrl_raw(*[_p(x) for x in a], ctypes.byref(tg), ctypes.c_double(grip_scale), _p(out))
+    return out
+
+
+def pd_joint_ctrl_raw(q6, v6, delta6, jnt_range12, ctrl_range12, kp6, kd6):
+    L = lib()
+    g = np.ascontiguousarray(np.concatenate([kp6, kd6]), dtype=np.float64)
+    a = [np.ascontiguousarray(x, dtype=np.float64).reshape(-1) for x in (q6, v6, delta6, jnt_range12, ctrl_range12)]
+    out = np.zeros(6)
+    L.ur3o_pd_joint_ctrl_raw(*[_p(x) for x in a], _p(g), _p(out))
+    return out
+
+
+def pinv3x6(J):
+    L = lib()
+    J = np.ascontiguousarray(J, dtype=np.float64).reshape(18)
+    P = np.zeros(18)
+    L.ur3o_pinv3x6(_p(J), _p(P))
+    return P.reshape(6, 3)
+
+
+def reward_v2(obs, act):
+    L = lib()
+    L.ur3o_reward_v2.restype = ctypes.c_double
+    o = np.ascontiguousarray(obs, dtype=np.float64)
+    a = np.ascontiguousarray(act, dtype=np.float64)
+    return L.ur3o_reward_v2(_p(o), _p(a))
+
+
+def philox(ctr, key):
+    L = lib()
+    c = (ctypes.c_uint * 4)(*ctr)
+    k = (ctypes.c_uint * 2)(*key)
+    o = (ctypes.c_uint * 4)()
+    L.ur3o_philox4x32(c, k, o)
+    return list(o)

@@ -1,0 +1,177 @@
+/*
+ * ur3e_oracle_batch.c — batched drivers over the scalar CPU oracle (TEST
+ * INFRASTRUCTURE ONLY).  These restate, env by env, exactly what one
+ * ur3e_batch_step() launch of the MI355X library computes, so tests can compare
+ * the two on the same inputs, and bench.py can time the oracle on the host
+ * cores (OpenMP over envs, static schedule) as the `cpu_baseline`.
+ *
+ * Semantics per env-step (task ids mirror include/ur3e_batch.h):
+ *   task 0 (gym ur3e-v2):  UR3eEnv2.step (gymnasium_env/envs/ur3e_env2.py:72-99)
+ *                          + SB3 VecEnv auto-reset on terminated|truncated.
+ *   task 1 (traj_l):       pid_task_ctrl on a [7] trajectory row + 1 mj_step
+ *                          (controller/move_l_mug.py:67-81).
+ *   task 2 (move_j):       pd_joint_ctrl on a [7] joint-target row + 1 mj_step
+ *                          (controller/move_j.py:76-86).
+ *   task 3 (ctrl):         raw ctrl row [nu] + frame_skip mj_step.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ur3e_oracle.h"
+
+typedef struct {
+  int task;
+  int frame_skip;
+  int max_episode_steps;
+  int auto_reset;
+  int reset_noise;
+  int reset_key;
+  double task_gains[12];
+  double joint_gains[12];
+  unsigned long long seed;
+  int env_id_offset;
+  int envs_per_block;
+} ur3o_config;
+
+static void gains_from_cfg(const ur3o_config* c, ur3o_task_gains* tg, ur3o_joint_gains* jg) {
+  for (int k = 0; k < 3; k++) {
+    tg->kp_pos[k] = c->task_gains[k];
+    tg->kd_pos[k] = c->task_gains[3 + k];
+    tg->kp_rot[k] = c->task_gains[6 + k];
+    tg->kd_rot[k] = c->task_gains[9 + k];
+  }
+  for (int k = 0; k < 6; k++) {
+    jg->kp[k] = c->joint_gains[k];
+    jg->kd[k] = c->joint_gains[6 + k];
+  }
+}
+
+/* reset one env to the configured keyframe (+ optional "high" mug noise), forward */
+static void env_reset(const ur3e_model_t* m, const ur3o_config* c, ur3o_env* e, double* obs) {
+  ur3o_data* d = &e->d;
+  ur3o_reset_data(m, d);
+  int key = c->reset_key;
+  if (key >= 0) {
+    for (int k = 0; k < m->nq; k++) d->qpos[k] = m->key_qpos[key][k];
+    for (int k = 0; k < m->nv; k++) d->qvel[k] = m->key_qvel[key][k];
+  }
+  if (c->reset_noise && m->id_body_fish >= 0) {
+    double u0 = ur3o_uniform01(e->seed, e->env_id, e->episode, 0);
+    double u1 = ur3o_uniform01(e->seed, e->env_id, e->episode, 1);
+    d->qpos[14] += 0.0 + (0.02 - 0.0) * u0;
+    d->qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+  }
+  ur3o_forward(m, d);
+  e->t = 0;
+  e->ep_return = 0;
+  e->ep_len = 0;
+  e->episode++;
+  if (obs && c->task == 0) ur3o_obs_v2(m, d, obs);
+}
+
+/* envs: array of n ur3o_env (opaque to python: allocate n*ur3o_sizeof_env()) */
+void ur3o_batch_init(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_env* envs, double* obs) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; i++) {
+    ur3o_env_init(m, &envs[i], c->seed, (unsigned int)(c->env_id_offset + i));
+    env_reset(m, c, &envs[i], obs ? obs + 24 * (size_t)i : 0);
+  }
+}
+
+void ur3o_batch_reset_one(const ur3e_model_t* m, const ur3o_config* c, ur3o_env* e, double* obs) {
+  env_reset(m, c, e, obs);
+}
+
+/* one env-step for all envs.  actions: [n][adim].  Outputs may be NULL. */
+void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_env* envs, const double* actions,
+                     int adim, double* obs, double* reward, unsigned char* terminated, unsigned char* truncated,
+                     double* terminal_obs) {
+  ur3o_task_gains tg;
+  ur3o_joint_gains jg;
+  gains_from_cfg(c, &tg, &jg);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; i++) {
+    ur3o_env* e = &envs[i];
+    ur3o_data* d = &e->d;
+    const double* a = actions + (size_t)adim * i;
+    double ctrl[UR3E_MAXU];
+    if (c->task == 0) {
+      double o[24], r;
+      int term, trunc;
+      ur3o_env_step_v2(m, e, &tg, a, c->frame_skip, o, &r, &term, &trunc);
+      if (c->max_episode_steps <= 0) trunc = 0;
+      else trunc = e->t >= c->max_episode_steps;
+      if (reward) reward[i] = r;
+      if (terminated) terminated[i] = (unsigned char)term;
+      if (truncated) truncated[i] = (unsigned char)trunc;
+      if ((term || trunc) && c->auto_reset) {
+        if (terminal_obs) memcpy(terminal_obs + 24 * (size_t)i, o, sizeof(o));
+        env_reset(m, c, e, obs ? obs + 24 * (size_t)i : 0);
+      } else if (obs) {
+        memcpy(obs + 24 * (size_t)i, o, sizeof(o));
+      }
+      continue;
+    }
+    if (c->task == 1) {
+      ur3o_pid_task_ctrl(m, d, a, &tg, ctrl);
+    } else if (c->task == 2) {
+      ur3o_move_j_ctrl(m, d, a, &jg, ctrl);
+    } else {
+      for (int k = 0; k < m->nu; k++) ctrl[k] = a[k];
+    }
+    for (int k = 0; k < m->nu; k++) d->ctrl[k] = ctrl[k];
+    int fs = c->task == 3 ? c->frame_skip : 1;
+    for (int s = 0; s < fs; s++) ur3o_step(m, d);
+    e->t += 1;
+  }
+}
+
+void ur3o_batch_get_state(const ur3e_model_t* m, int n, const ur3o_env* envs, double* qpos, double* qvel,
+                          double* warm, int* ncon) {
+  for (int i = 0; i < n; i++) {
+    const ur3o_data* d = &envs[i].d;
+    if (qpos) memcpy(qpos + (size_t)m->nq * i, d->qpos, sizeof(double) * m->nq);
+    if (qvel) memcpy(qvel + (size_t)m->nv * i, d->qvel, sizeof(double) * m->nv);
+    if (warm) memcpy(warm + (size_t)m->nv * i, d->qacc_warmstart, sizeof(double) * m->nv);
+    if (ncon) ncon[i] = d->ncon;
+  }
+}
+
+void ur3o_batch_set_state(const ur3e_model_t* m, int n, ur3o_env* envs, const double* qpos, const double* qvel,
+                          const double* warm) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; i++) {
+    ur3o_data* d = &envs[i].d;
+    memcpy(d->qpos, qpos + (size_t)m->nq * i, sizeof(double) * m->nq);
+    memcpy(d->qvel, qvel + (size_t)m->nv * i, sizeof(double) * m->nv);
+    if (warm) memcpy(d->qacc_warmstart, warm + (size_t)m->nv * i, sizeof(double) * m->nv);
+    ur3o_forward(m, d);
+  }
+}
+
+/* diagnostics for tests */
+void ur3o_env_diag(const ur3o_env* e, int* ncon, int* nefc, int* niter, double* touch) {
+  *ncon = e->d.ncon;
+  *nefc = e->d.nefc;
+  *niter = e->d.solver_niter;
+  for (int k = 0; k < UR3E_MAXTOUCH; k++) touch[k] = e->d.touch[k];
+}
+
+/* single-env helpers for golden-vector tests */
+void ur3o_forward_state(const ur3e_model_t* m, const double* qpos, const double* qvel, double* site_xpos,
+                        double* site_xmat, double* qfrc_bias, double* qM, int* ncon) {
+  ur3o_data* d = (ur3o_data*)malloc(sizeof(ur3o_data));
+  ur3o_reset_data(m, d);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  ur3o_forward(m, d);
+  if (site_xpos) memcpy(site_xpos, d->site_xpos, sizeof(double) * 3 * m->nsite);
+  if (site_xmat) memcpy(site_xmat, d->site_xmat, sizeof(double) * 9 * m->nsite);
+  if (qfrc_bias) memcpy(qfrc_bias, d->qfrc_bias, sizeof(double) * m->nv);
+  if (qM)
+    for (int i = 0; i < m->nv; i++)
+      for (int j = 0; j < m->nv; j++) qM[i * m->nv + j] = d->qM[i][j];
+  if (ncon) *ncon = d->ncon;
+  free(d);
+}
