@@ -1,0 +1,195 @@
+"""Benchmark: env-steps/sec of the batched UR3e gym step on MI355X.
+
+Workload (BASELINE.json configs[3], per GPU): `assets/main.xml` (arm + 2F-85 +
+mug, contacts on), gymnasium `ur3e-v2` step semantics (pid_task_ctrl + 2
+physics substeps + obs/reward/termination + auto-reset at T=2500), uniformly
+random task-space actions in the v2 action Box, 4096 envs per GPU.  One
+"step" = one env-step of all resident envs = one launch of k_env_step.
+
+Multi-GPU: one process per GPU (torchrun), envs sharded by contiguous global
+id (weak scaling: 4096 per GPU), per-step RCCL gather of (obs, reward, done)
+to rank 0 (the policy rank) as the north_star's C4 prescribes.
+
+Prints ONE JSON line on rank 0 (see the contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+# algorithmic HBM bytes per env-step for main.xml (nq 21, nv 20, n_a 4, n_obs 24)
+ALGO_BYTES_PER_ENV_STEP = 1898
+
+
+def cpu_baseline(n_envs_sample=128, steps=20, seed=0):
+    """Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of the same workload."""
+    from oracle import pyoracle as po
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model("main")
+    c = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=seed)
+    oc = po.OracleConfig()
+    for f, _ in po.OracleConfig._fields_:
+        v = getattr(c, f)
+        if f in ("task_gains", "joint_gains"):
+            for k in range(12):
+                getattr(oc, f)[k] = v[k]
+        else:
+            setattr(oc, f, v)
+    ob = po.OracleBatch(mc, oc, n_envs_sample)
+    rng = np.random.default_rng(seed)
+    lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
+    hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
+    acts = [rng.uniform(lo, hi, size=(n_envs_sample, 4)) for _ in range(steps)]
+    ob.step(acts[0])
+    t0 = time.perf_counter()
+    for a in acts:
+        ob.step(a)
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=cores, kind="port",
+                sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps), "
+                       f"oracle/ C restatement, OpenMP {cores} threads, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--envs-per-block", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-envs", type=int, default=128)
+    ap.add_argument("--cpu-sample-steps", type=int, default=20)
+    ap.add_argument("--no-gather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from ur3e_amd import runtime as rt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    n = args.envs_per_gpu
+    md, mc = rt.load_model("main")
+    cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=1234,
+                         env_id_offset=rank * n, envs_per_block=args.envs_per_block)
+    batch = rt.Batch(mc, cfg, n, device=local)
+    lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
+    hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+
+    gather = world > 1 and not args.no_gather
+    if gather:
+        payload = torch.empty((n, 26), dtype=torch.float64, device=dev)
+        glist = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+
+    def one_step():
+        a = lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device=dev, generator=gen)
+        obs, rew, term, trunc, _ = batch.step(a)
+        if gather:
+            payload[:, :24] = obs
+            payload[:, 24] = rew
+            payload[:, 25] = (term | trunc).to(torch.float64)
+            dist.gather(payload, glist, dst=0)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    kernel_ms = []
+    for i in range(args.steps):
+        one_step()
+        if i == args.steps - 1 or (i % 10 == 0 and rank == 0 and i > 0):
+            pass
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    # dominant kernel duration: HIP events recorded by the library around its last k_env_step launch
+    step_kernel_ms = batch.last_step_ms()
+    ev_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    # per-kernel average over the timed region from the stream events (launch gaps included)
+    kernel_avg_ms = ev_ms / args.steps
+    ms_per_step = wall * 1000.0 / args.steps
+    total_env_steps = n * world * args.steps
+    value = total_env_steps / wall
+
+    if rank == 0:
+        achieved = ALGO_BYTES_PER_ENV_STEP * n / (step_kernel_ms * 1e-3) / 1e9
+        prof_traffic = None
+        tf = os.path.join(REPO, "profiles", "traffic_r01.json")
+        if os.path.exists(tf):
+            try:
+                with open(tf) as f:
+                    prof_traffic = json.load(f).get("hbm_bytes_per_launch")
+            except Exception:
+                prof_traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
+            except Exception as e:  # the oracle is only the checker; never fail the bench on it
+                cpu = dict(value=None, unit="env-steps/s", cores=None, kind="port", sample=f"failed: {e}")
+        line = {
+            "metric": "env-steps/sec at N parallel envs, 1/2/4/8 MI355X; max |qpos-ref| @1k steps",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform random actions in the ur3e-v2 action Box; stochastic 'high' mug resets)",
+            "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
+                       "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
+                       "envs_per_block": batch.cfg.envs_per_block if batch.cfg.envs_per_block else 16,
+                       "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic,
+                         "kernel": "k_env_step", "kernel_ms": step_kernel_ms,
+                         "stream_avg_ms": kernel_avg_ms,
+                         "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                         "note": "path is FP64-latency-bound (SURVEY.md §8d); HBM fraction reported as required"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    batch.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

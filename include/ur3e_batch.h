@@ -1,0 +1,111 @@
+/*
+ * ur3e_batch.h — C ABI of the MI355X-native batched UR3e step library
+ * (ur3e_amd/_lib/libur3e_amd.so, built from ur3e_amd/csrc/ur3e_batch.hip).
+ *
+ * One handle = N environments resident in HBM on one GPU.  Every pointer
+ * argument named d_* is a DEVICE pointer (e.g. a torch tensor's data_ptr() on
+ * the same device); `stream` is a hipStream_t (NULL = default stream).  All
+ * calls only enqueue work on `stream` and return immediately.  Return value: 0
+ * on success, a negative UR3E_E* code otherwise; ur3e_last_error() gives a
+ * thread-local message.  A handle is not thread-safe.
+ *
+ * Reference interfaces each entry point replaces (the reference's boundary is
+ * Python — gymnasium Env + MuJoCo C API):
+ *
+ *   ur3e_batch_create   MujocoEnv.__init__ / UR3eEnv2.__init__
+ *                       (gymnasium_env/envs/ur3e_env2.py:30-70) × N processes of
+ *                       SubprocVecEnv (gymnasium_src/scripts/regular_rl/rl/train_rl.py:38-44)
+ *   ur3e_batch_reset    MujocoEnv.reset -> mj_resetData -> UR3eEnv2.reset_model
+ *                       (ur3e_env2.py:101-109; utils/gym_utils.py:63-79)
+ *   ur3e_batch_step     UR3eEnv2.step (ur3e_env2.py:72-99) = pid_task_ctrl
+ *                       (controller/controller_func.py:68-117) + do_simulation ->
+ *                       mj_step × frame_skip + _get_obs + compute_reward +
+ *                       termination/truncation, with SB3 VecEnv auto-reset; for the
+ *                       scripted tasks: controller/move_l_mug.py:67-81 (traj_l),
+ *                       controller/move_j.py:76-86 (move_j)
+ *   ur3e_batch_get_state / ur3e_batch_set_state
+ *                       MjData.qpos/qvel/qacc_warmstart read/write + mj_forward
+ *                       (MujocoEnv.set_state; utils/utils.py:15-24)
+ *   ur3e_batch_destroy  env.close()
+ */
+#ifndef UR3E_BATCH_H
+#define UR3E_BATCH_H
+
+#include <stdint.h>
+
+#include "ur3e_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UR3E_ABI_VERSION 1
+
+/* tasks (what one env-step means) */
+#define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
+#define UR3E_TASK_TRAJ_L 1  /* action [N,7] task-space trajectory row: pid_task_ctrl */
+#define UR3E_TASK_MOVE_J 2  /* action [N,7] joint targets + grip: move_j PD */
+#define UR3E_TASK_CTRL 3    /* action [N,nu] raw actuator controls */
+
+/* error codes */
+#define UR3E_OK 0
+#define UR3E_EINVAL -1
+#define UR3E_EHIP -2
+#define UR3E_ENOMEM -3
+#define UR3E_EMODEL -4
+
+typedef struct ur3e_config_t {
+  int task;
+  int frame_skip;        /* physics substeps per env-step (gym ur3e-v2: 2) */
+  int max_episode_steps; /* truncation horizon (ur3e-v2: 2500); <= 0: never */
+  int auto_reset;        /* SB3 VecEnv semantics on terminated|truncated */
+  int reset_noise;       /* 1: gym_utils.get_mug_xpos_noise("high") on reset */
+  int reset_key;         /* keyframe index used by reset (-1: qpos0) */
+  double task_gains[12]; /* kp_pos[3], kd_pos[3], kp_rot[3], kd_rot[3] (config_l_mug.yml) */
+  double joint_gains[12];/* kp[6], kd[6] (config_j.yml) */
+  unsigned long long seed; /* Philox key for reset noise */
+  int env_id_offset;     /* global id of local env 0 (multi-GPU shards) */
+  int envs_per_block;    /* lanes used per 64-wide wavefront (1..64; 0 = auto) */
+} ur3e_config_t;
+
+typedef struct ur3e_batch ur3e_batch_t;
+
+int ur3e_abi_version(void);
+const char* ur3e_last_error(void);
+
+int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
+                      ur3e_batch_t** out);
+int ur3e_batch_destroy(ur3e_batch_t* b);
+
+/* reset envs whose d_mask[i] != 0 (d_mask NULL: all); writes obs rows of reset envs */
+int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* d_obs, void* stream);
+
+/* one env-step for all envs.  d_actions [N, adim] row-major.  Outputs may be NULL:
+   d_obs [N,24], d_reward [N], d_terminated/d_truncated [N] u8, d_terminal_obs [N,24]
+   (rows written only for envs that finished this step; d_obs then holds the reset obs). */
+int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adim, double* d_obs, double* d_reward,
+                    uint8_t* d_terminated, uint8_t* d_truncated, double* d_terminal_obs, void* stream);
+
+/* state in user layout: d_qpos [N,nq], d_qvel [N,nv], d_warm [N,nv] (any may be NULL) */
+int ur3e_batch_get_state(ur3e_batch_t* b, double* d_qpos, double* d_qvel, double* d_warm, void* stream);
+/* sets state then runs the forward pass (refreshes the stale-kinematics carry) */
+int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const double* d_qvel, const double* d_warm,
+                         void* stream);
+/* diagnostics: d_ncon [N] contacts of the last forward, d_ep_len [N], d_ep_return [N],
+   d_nwarn [N] bad-value auto-resets (each may be NULL) */
+int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, double* d_ep_return, int* d_nwarn,
+                        void* stream);
+
+/* sizes */
+int ur3e_batch_num_envs(const ur3e_batch_t* b);
+int ur3e_batch_nq(const ur3e_batch_t* b);
+int ur3e_batch_nv(const ur3e_batch_t* b);
+int ur3e_batch_nu(const ur3e_batch_t* b);
+
+/* profiling: events recorded around the most recent step kernel on its stream */
+int ur3e_batch_last_step_ms(ur3e_batch_t* b, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UR3E_BATCH_H */

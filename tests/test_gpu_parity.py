@@ -1,0 +1,112 @@
+"""GPU parity: the MI355X library (through its C ABI) vs the CPU oracle, same
+seeded inputs.  The bar is bit-exactness: both sides run the same FP64
+operation order with contraction off and deterministic transcendentals, so
+qpos/qvel/obs/reward and the integer contact counts must match exactly.
+(The north_star tolerance, |dqpos| <= 1e-5 after 1000 steps, is checked too,
+but exact equality is what these tests require.)"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _oracle_cfg(po, c):
+    oc = po.OracleConfig()
+    for f, _ in po.OracleConfig._fields_:
+        v = getattr(c, f)
+        if f in ("task_gains", "joint_gains"):
+            for k in range(12):
+                getattr(oc, f)[k] = v[k]
+        else:
+            setattr(oc, f, v)
+    return oc
+
+
+def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=16, check_every=1):
+    torch = _torch()
+    from oracle import pyoracle as po
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model(model_name)
+    cfg = rt.make_config(task=task, frame_skip=frame_skip, model=md, seed=seed, envs_per_block=epb,
+                         reset_noise=(model_name == "main"),
+                         reset_key=md["id_key_down"] if md["id_key_down"] >= 0 else -1)
+    gb = rt.Batch(mc, cfg, n)
+    ob = po.OracleBatch(mc, _oracle_cfg(po, cfg), n)
+    gobs = gb.obs.cpu().numpy()
+    if task == rt.TASK_GYM_V2:
+        np.testing.assert_array_equal(gobs, ob.obs)
+    rng = np.random.default_rng(seed)
+    max_dq = 0.0
+    for s in range(steps):
+        a = action_fn(rng, n, md)
+        o_obs, o_rew, o_term, o_trunc, o_tobs = ob.step(a)
+        g_obs, g_rew, g_term, g_trunc, g_tobs = gb.step(torch.from_numpy(a))
+        if s % check_every == 0 or s == steps - 1:
+            torch.cuda.synchronize()
+            if task == rt.TASK_GYM_V2:
+                np.testing.assert_array_equal(g_rew.cpu().numpy(), o_rew, err_msg=f"reward step {s}")
+                np.testing.assert_array_equal(g_term.cpu().numpy(), o_term, err_msg=f"terminated step {s}")
+                np.testing.assert_array_equal(g_trunc.cpu().numpy(), o_trunc, err_msg=f"truncated step {s}")
+                np.testing.assert_array_equal(g_obs.cpu().numpy(), o_obs, err_msg=f"obs step {s}")
+            qp, qv, wa = gb.get_state()
+            oqp, oqv, owa, onc = ob.get_state()
+            max_dq = max(max_dq, float(np.abs(qp.cpu().numpy() - oqp).max()))
+            np.testing.assert_array_equal(qp.cpu().numpy(), oqp, err_msg=f"qpos step {s}")
+            np.testing.assert_array_equal(qv.cpu().numpy(), oqv, err_msg=f"qvel step {s}")
+            np.testing.assert_array_equal(wa.cpu().numpy(), owa, err_msg=f"warmstart step {s}")
+            info = gb.get_info()
+            np.testing.assert_array_equal(info["ncon"].cpu().numpy(), onc, err_msg=f"ncon step {s}")
+    assert max_dq <= 1e-5
+    gb.close()
+    return ob
+
+
+def _gym_actions(rng, n, md):
+    lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
+    hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
+    return rng.uniform(lo, hi, size=(n, 4))
+
+
+def test_gym_v2_random_actions_short():
+    _run_pair("main", 0, 64, 60, _gym_actions)
+
+
+def test_gym_v2_grasp_region():
+    # actions concentrated around the mug with the gripper closing: exercises pad-box contacts
+    def act(rng, n, md):
+        a = np.zeros((n, 4))
+        a[:, 0] = 0.29799994 + rng.normal(size=n) * 0.01
+        a[:, 1] = 0.13349916 + rng.normal(size=n) * 0.01
+        a[:, 2] = rng.uniform(0.02, 0.12, size=n)
+        a[:, 3] = rng.uniform(0.5, 1.0, size=n)
+        return a
+    _run_pair("main", 0, 64, 150, act, seed=3)
+
+
+def test_move_j_2f85():
+    def act(rng, n, md):
+        q0 = np.array(md["key_qpos"][md["id_key_down"]][:6])
+        a = np.zeros((n, 7))
+        a[:, :6] = q0 + rng.uniform(-0.5, 0.5, size=(n, 6))
+        a[:, 6] = rng.uniform(0, 1, size=n)
+        return a
+    _run_pair("ur3e_2f85", 2, 64, 100, act)
+
+
+def test_ctrl_raw():
+    def act(rng, n, md):
+        return rng.uniform(-20, 20, size=(n, 6))
+    _run_pair("ur3e_raw", 3, 32, 100, act, frame_skip=1)
+
+
+@pytest.mark.slow
+def test_gym_v2_1000_steps():
+    """north_star: qpos within 1e-5 after 1000 steps (here: bit-exact)."""
+    _run_pair("main", 0, 128, 1000, _gym_actions, check_every=100)

@@ -1,0 +1,656 @@
+/*
+ * ur3e_batch.hip — MI355X (gfx950) batched UR3e environment: kernels + C ABI.
+ *
+ * One fused kernel per env-step (k_env_step): controller -> frame_skip physics
+ * substeps -> observation / reward / termination -> in-kernel SB3 auto-reset.
+ * One environment per wavefront lane; `envs_per_block` lanes of each 64-wide
+ * wavefront are populated, trading lane packing for CU coverage (at 4096 envs
+ * 16 envs/wave puts one wave on every one of the 256 CUs).
+ *
+ * Persistent per-env state lives in HBM structure-of-arrays ([field][env]) so
+ * a wave's 64 lanes touch consecutive doubles: qpos[nq], qvel[nv],
+ * qacc_warmstart[nv], the stale-kinematics carry[54] (tcp pose, arm Jacobian,
+ * qfrc_bias[0:6] of the last forward pass — MuJoCo's post-mj_step mjData
+ * semantics that the reference controller and observation read), and episode
+ * counters.  User-facing tensors (actions, obs, get/set_state) are row-major.
+ *
+ * Reference behaviour restated (file:line in /root/reference):
+ *   UR3eEnv2.step / reset_model / _get_obs / compute_reward / _check_termination
+ *     gymnasium_env/envs/ur3e_env2.py:72-261
+ *   pid_task_ctrl / pd_joint_ctrl     controller/controller_func.py:68-167
+ *   move_j                            controller/move_j.py:14-38
+ *   predicates                        utils/gym_utils.py:8-172
+ *   mj_step (MuJoCo 3.3.3)            ur3e_engine.h
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/ur3e_batch.h"
+#include "ur3e_engine.h"
+
+#define NCARRY 54
+
+/* ================================================================== */
+/* scipy Rotation semantics (controller_func.get_rot_err)              */
+/* ================================================================== */
+KD void k_quat_from_matrix(const double mt[9], double q[4]) {
+  double dec[4] = {mt[0], mt[4], mt[8], mt[0] + mt[4] + mt[8]};
+  int ch = 0;
+  for (int k = 1; k < 4; k++)
+    if (dec[k] > dec[ch]) ch = k;
+  if (ch != 3) {
+    int i = ch, j = (i + 1) % 3, k = (j + 1) % 3;
+    q[i] = 1 - dec[3] + 2 * mt[3 * i + i];
+    q[j] = mt[3 * j + i] + mt[3 * i + j];
+    q[k] = mt[3 * k + i] + mt[3 * i + k];
+    q[3] = mt[3 * k + j] - mt[3 * j + k];
+  } else {
+    q[0] = mt[7] - mt[5];
+    q[1] = mt[2] - mt[6];
+    q[2] = mt[3] - mt[1];
+    q[3] = 1 + dec[3];
+  }
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+
+KD void k_quat_from_rotvec(const double rv[3], double q[4]) {
+  double ang = sqrt(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
+  double sc;
+  if (ang <= 1e-3) {
+    double a2 = ang * ang;
+    sc = 0.5 - a2 / 48 + a2 * a2 / 3840;
+  } else {
+    sc = ur3e_sin(ang / 2) / ang;
+  }
+  q[0] = sc * rv[0]; q[1] = sc * rv[1]; q[2] = sc * rv[2];
+  q[3] = ur3e_cos(ang / 2);
+}
+
+KD void k_rotvec_from_quat(const double qin[4], double rv[3]) {
+  double q[4] = {qin[0], qin[1], qin[2], qin[3]};
+  if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+  double ang = 2 * ur3e_atan2(sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]), q[3]);
+  double sc;
+  if (ang <= 1e-3) {
+    double a2 = ang * ang;
+    sc = 2 + a2 / 12 + 7 * a2 * a2 / 2880;
+  } else {
+    sc = ang / ur3e_sin(ang / 2);
+  }
+  rv[0] = sc * q[0]; rv[1] = sc * q[1]; rv[2] = sc * q[2];
+}
+
+KD void k_rot_err(const double xmat[9], const double target[3], double err[3]) {
+  double q[4], qd[4], qi[4], r[4];
+  k_quat_from_matrix(xmat, q);
+  k_quat_from_rotvec(target, qd);
+  qi[0] = -q[0]; qi[1] = -q[1]; qi[2] = -q[2]; qi[3] = q[3];
+  double cr[3];
+  k_cross3(cr, qd, qi);
+  r[0] = qd[3] * qi[0] + qi[3] * qd[0] + cr[0];
+  r[1] = qd[3] * qi[1] + qi[3] * qd[1] + cr[1];
+  r[2] = qd[3] * qi[2] + qi[3] * qd[2] + cr[2];
+  r[3] = qd[3] * qi[3] - qd[0] * qi[0] - qd[1] * qi[1] - qd[2] * qi[2];
+  k_rotvec_from_quat(r, err);
+}
+
+/* ================================================================== */
+/* controllers                                                         */
+/* ================================================================== */
+struct KGains {
+  double task[12];
+  double joint[12];
+};
+
+/* pid_task_ctrl (controller_func.py:68-117): carry = [tcp_xpos 3, tcp_xmat 9, J 36, bias 6] */
+KD void k_pid_task_ctrl(const double traj[7], const double* carry, const double qv[6], const KGains& g,
+                        double grip_scale, double ctrl[7]) {
+  const double* tcp_xpos = carry;
+  const double* tcp_xmat = carry + 3;
+  const double* J = carry + 12;
+  const double* bias = carry + 48;
+  double ep[3] = {traj[0] - tcp_xpos[0], traj[1] - tcp_xpos[1], traj[2] - tcp_xpos[2]};
+  double er[3];
+  k_rot_err(tcp_xmat, traj + 3, er);
+  double jv[6];
+  for (int r = 0; r < 6; r++) {
+    double s = 0;
+    for (int k = 0; k < 6; k++) s += J[6 * r + k] * qv[k];
+    jv[r] = s;
+  }
+  double u[6];
+  for (int r = 0; r < 3; r++) u[r] = g.task[r] * ep[r] - g.task[3 + r] * jv[r];
+  for (int r = 0; r < 3; r++) u[3 + r] = g.task[6 + r] * er[r] - g.task[9 + r] * jv[3 + r];
+  for (int c = 0; c < 6; c++) {
+    double s = 0;
+    for (int r = 0; r < 6; r++) s += J[6 * r + c] * u[r];
+    ctrl[c] = s + bias[c];
+  }
+  ctrl[6] = traj[6] * grip_scale;
+}
+
+/* move_j = pd_joint_ctrl on delta = target - q (move_j.py:14-38, controller_func.py:128-167) */
+KD void k_move_j_ctrl(KModel m, const KData* d, const double traj[7], const KGains& g, double* ctrl) {
+  for (int k = 0; k < 6; k++) {
+    double q = d->qpos[k];
+    double delta = traj[k] - q;
+    double t = q + delta;
+    if (t < m->jnt_range[k][0]) t = m->jnt_range[k][0];
+    if (t > m->jnt_range[k][1]) t = m->jnt_range[k][1];
+    double e = t - q;
+    double uk = g.joint[k] * e + g.joint[6 + k] * (-d->qvel[k]);
+    if (uk < m->act_ctrlrange[k][0]) uk = m->act_ctrlrange[k][0];
+    if (uk > m->act_ctrlrange[k][1]) uk = m->act_ctrlrange[k][1];
+    ctrl[k] = uk;
+  }
+  if (m->nu > 6) ctrl[6] = traj[6] * m->act_ctrlrange[m->nu - 1][1];
+}
+
+/* ================================================================== */
+/* stale-kinematics carry + UR3eEnv2 epilogue                          */
+/* ================================================================== */
+KD void k_make_carry(KModel m, const KData* d, double* carry) {
+  int s = m->id_site_tcp;
+  if (s < 0) {
+    for (int k = 0; k < NCARRY; k++) carry[k] = 0;
+    return;
+  }
+  for (int k = 0; k < 3; k++) carry[k] = d->site_xpos[s][k];
+  for (int k = 0; k < 9; k++) carry[3 + k] = d->site_xmat[s][k];
+  double jp[3][K_NV], jr[3][K_NV];
+  k_jac_point(m, d, m->site_bodyid[s], d->site_xpos[s], jp, jr);
+  for (int c = 0; c < 6; c++) {
+    for (int r = 0; r < 3; r++) {
+      carry[12 + 6 * r + c] = jp[r][c];
+      carry[12 + 6 * (3 + r) + c] = jr[r][c];
+    }
+  }
+  for (int k = 0; k < 6; k++) carry[48 + k] = d->qfrc_bias[k];
+}
+
+KD int k_block_grasp_state(KModel m, const KData* d) {
+  int lp = 0, rp = 0;
+  for (int ci = 0; ci < d->ncon; ci++) {
+    int b1 = m->geom_bodyid[d->contact[ci].geom1], b2 = m->geom_bodyid[d->contact[ci].geom2];
+    int fish = (b1 == m->id_body_fish || b2 == m->id_body_fish);
+    if (!fish) continue;
+    if (b1 == m->id_body_lpad || b2 == m->id_body_lpad) lp = 1;
+    if (b1 == m->id_body_rpad || b2 == m->id_body_rpad) rp = 1;
+  }
+  return lp + rp;
+}
+
+KD int k_self_collision(KModel m, const KData* d) {
+  for (int ci = 0; ci < d->ncon; ci++) {
+    int b1 = m->geom_bodyid[d->contact[ci].geom1], b2 = m->geom_bodyid[d->contact[ci].geom2];
+    int a1 = (m->mask_arm_bodies >> b1) & 1, a2 = (m->mask_arm_bodies >> b2) & 1;
+    if (a1 && a2) {
+      int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+      if (g1 && g2) continue;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+KD void k_obs_v2(KModel m, const KData* d, double obs[24]) {
+  int st = m->id_site_tcp, sh = m->id_site_handle, gb = m->id_body_ghost;
+  const double* tcp = d->site_xpos[st];
+  const double* mug = d->site_xpos[sh];
+  const double* gh = d->xpos[gb];
+  double vt[6], vh[6];
+  k_site_velocity(m, d, st, vt);
+  k_site_velocity(m, d, sh, vh);
+  for (int k = 0; k < 3; k++) {
+    obs[k] = tcp[k];
+    obs[3 + k] = mug[k];
+    obs[6 + k] = gh[k];
+    obs[9 + k] = tcp[k] - mug[k];
+    obs[12 + k] = mug[k] - gh[k];
+    obs[15 + k] = vt[3 + k];
+    obs[18 + k] = vt[3 + k] - vh[3 + k];
+  }
+  obs[21] = d->qpos[6];
+  obs[22] = d->qvel[6];
+  int gs = k_block_grasp_state(m, d);
+  int robust = 0;
+  if (gs == 2) {
+    double dx = fabs(tcp[0] - mug[0]), dy = fabs(tcp[1] - mug[1]), dz = fabs(tcp[2] - mug[2]);
+    robust = (dx < 0.01 && dy < 0.005 && dz < 0.05);
+  }
+  obs[23] = (double)robust;
+}
+
+KD double k_reward_v2(const double obs[24], const double act[4]) {
+  double mug_z = obs[5];
+  const double* g2m = obs + 9;
+  const double* m2t = obs + 12;
+  const double* gv = obs + 15;
+  double grasped = obs[23];
+  double grip = act[3];
+  double xy = sqrt(g2m[0] * g2m[0] + g2m[1] * g2m[1]);
+  double zerr = fabs(g2m[2] - 0.02);
+  double place = sqrt(m2t[0] * m2t[0] + m2t[1] * m2t[1] + m2t[2] * m2t[2]);
+  double ready = ur3e_exp(-10 * xy) * ur3e_exp(-20 * zerr);
+  double align = 2.0 * ready;
+  double grasp_act = 2.0 * grip * ready;
+  double grasp_ach = 10.0 * grasped * ready;
+  double lift = 8.0 * grasped * ur3e_tanh(8.0 * (mug_z > 0 ? mug_z : 0));
+  double placement = grasped * (4.0 * ur3e_exp(-15 * place) - 1.5 * place);
+  double success = 0.0;
+  if (grasped != 0 && place < 0.05) success = 50.0;
+  double pen = 0.0;
+  pen += -1.0 * (-g2m[2] > 0 ? -g2m[2] : 0);
+  pen += -0.01 * sqrt(gv[0] * gv[0] + gv[1] * gv[1] + gv[2] * gv[2]);
+  return align + grasp_act + grasp_ach + lift + placement + success + pen;
+}
+
+KD int k_termination_v2(KModel m, const KData* d, const double obs[24]) {
+  double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
+  if (1.0 < sqrt(dx * dx + dy * dy + dz * dz)) return 1;
+  if (k_self_collision(m, d)) return 1;
+  if (obs[5] <= m->fish_topple_z) return 1;
+  return 0;
+}
+
+/* ================================================================== */
+/* Philox4x32-10 (counter = env id, episode, draw, tag; key = seed)    */
+/* ================================================================== */
+KD double k_uniform01(unsigned long long seed, unsigned int env_id, unsigned int episode, unsigned int k) {
+  unsigned int c0 = env_id, c1 = episode, c2 = k, c3 = 0x55523345u;
+  unsigned int k0 = (unsigned int)seed, k1 = (unsigned int)(seed >> 32);
+  for (int r = 0; r < 10; r++) {
+    unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+    unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+    unsigned int hi0 = (unsigned int)(p0 >> 32), lo0 = (unsigned int)p0;
+    unsigned int hi1 = (unsigned int)(p1 >> 32), lo1 = (unsigned int)p1;
+    unsigned int n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  unsigned long long bits = ((unsigned long long)c0 << 32) | c1;
+  return (double)(bits >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* ================================================================== */
+/* device state                                                        */
+/* ================================================================== */
+struct KState {
+  int n;
+  double* qpos;   /* [nq][n] */
+  double* qvel;   /* [nv][n] */
+  double* warm;   /* [nv][n] */
+  double* carry;  /* [NCARRY][n] */
+  int* t;
+  unsigned int* episode;
+  int* ep_len;
+  double* ep_return;
+  int* ncon;
+  int* nwarn;
+};
+
+struct KConfig {
+  int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
+  unsigned long long seed;
+  int env_id_offset;
+  int epb;
+  KGains gains;
+};
+
+KD void k_load(KModel m, const KState& s, int e, KData* d) {
+  const int n = s.n;
+  for (int k = 0; k < m->nq; k++) d->qpos[k] = s.qpos[(size_t)k * n + e];
+  for (int k = 0; k < m->nv; k++) d->qvel[k] = s.qvel[(size_t)k * n + e];
+  for (int k = 0; k < m->nv; k++) d->qacc_warmstart[k] = s.warm[(size_t)k * n + e];
+  d->nwarn = s.nwarn[e];
+}
+
+KD void k_store(KModel m, const KState& s, int e, const KData* d, const double* carry) {
+  const int n = s.n;
+  for (int k = 0; k < m->nq; k++) s.qpos[(size_t)k * n + e] = d->qpos[k];
+  for (int k = 0; k < m->nv; k++) s.qvel[(size_t)k * n + e] = d->qvel[k];
+  for (int k = 0; k < m->nv; k++) s.warm[(size_t)k * n + e] = d->qacc_warmstart[k];
+  for (int k = 0; k < NCARRY; k++) s.carry[(size_t)k * n + e] = carry[k];
+  s.ncon[e] = d->ncon;
+  s.nwarn[e] = d->nwarn;
+}
+
+/* reset one env in registers/scratch: keyframe (+ mug noise), forward, obs, carry */
+KD void k_reset_env(KModel m, const KConfig& c, const KState& s, int e, KData* d, double obs[24],
+                    double carry[NCARRY]) {
+  for (int k = 0; k < m->nq; k++) d->qpos[k] = m->qpos0[k];
+  for (int k = 0; k < m->nv; k++) { d->qvel[k] = 0; d->qacc_warmstart[k] = 0; }
+  for (int k = 0; k < m->nu; k++) d->ctrl[k] = 0;
+  if (c.reset_key >= 0) {
+    for (int k = 0; k < m->nq; k++) d->qpos[k] = m->key_qpos[c.reset_key][k];
+    for (int k = 0; k < m->nv; k++) d->qvel[k] = m->key_qvel[c.reset_key][k];
+  }
+  unsigned int ep = s.episode[e];
+  if (c.reset_noise && m->id_body_fish >= 0) {
+    unsigned int gid = (unsigned int)(c.env_id_offset + e);
+    double u0 = k_uniform01(c.seed, gid, ep, 0);
+    double u1 = k_uniform01(c.seed, gid, ep, 1);
+    d->qpos[14] += 0.0 + (0.02 - 0.0) * u0;
+    d->qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+  }
+  d->nwarn = 0;
+  k_forward(m, d);
+  s.t[e] = 0;
+  s.ep_len[e] = 0;
+  s.ep_return[e] = 0;
+  s.episode[e] = ep + 1;
+  if (c.task == UR3E_TASK_GYM_V2) k_obs_v2(m, d, obs);
+  k_make_carry(m, d, carry);
+}
+
+KD int k_env_index(const KConfig& c, int n) {
+  int lane = threadIdx.x;
+  if (lane >= c.epb) return -1;
+  int e = blockIdx.x * c.epb + lane;
+  return e < n ? e : -1;
+}
+
+__global__ __launch_bounds__(64) void k_env_reset(const ur3e_model_t* __restrict__ m, KConfig c, KState s,
+                                                  const unsigned char* __restrict__ mask,
+                                                  double* __restrict__ obs_out) {
+  int e = k_env_index(c, s.n);
+  if (e < 0) return;
+  if (mask && !mask[e]) return;
+  KData d;
+  double obs[24], carry[NCARRY];
+  k_reset_env(m, c, s, e, &d, obs, carry);
+  k_store(m, s, e, &d, carry);
+  if (obs_out && c.task == UR3E_TASK_GYM_V2)
+    for (int k = 0; k < 24; k++) obs_out[(size_t)e * 24 + k] = obs[k];
+}
+
+__global__ __launch_bounds__(64) void k_env_step(const ur3e_model_t* __restrict__ m, KConfig c, KState s,
+                                                 const double* __restrict__ actions, int adim,
+                                                 double* __restrict__ obs_out, double* __restrict__ rew_out,
+                                                 unsigned char* __restrict__ term_out,
+                                                 unsigned char* __restrict__ trunc_out,
+                                                 double* __restrict__ tobs_out) {
+  int e = k_env_index(c, s.n);
+  if (e < 0) return;
+  const int n = s.n;
+  KData d;
+  k_load(m, s, e, &d);
+  double a[8];
+  for (int k = 0; k < adim && k < 8; k++) a[k] = actions[(size_t)e * adim + k];
+  double ctrl[K_NU];
+  double carry[NCARRY];
+  if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
+    for (int k = 0; k < NCARRY; k++) carry[k] = s.carry[(size_t)k * n + e];
+    double traj[7];
+    if (c.task == UR3E_TASK_GYM_V2) {
+      traj[0] = a[0]; traj[1] = a[1]; traj[2] = a[2];
+      traj[3] = -1.209; traj[4] = -1.209; traj[5] = 1.209;
+      traj[6] = a[3];
+    } else {
+      for (int k = 0; k < 7; k++) traj[k] = a[k];
+    }
+    double out[7];
+    k_pid_task_ctrl(traj, carry, d.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
+    for (int k = 0; k < 6; k++) ctrl[k] = out[k];
+    if (m->nu > 6) ctrl[6] = out[6];
+  } else if (c.task == UR3E_TASK_MOVE_J) {
+    k_move_j_ctrl(m, &d, a, c.gains, ctrl);
+  } else {
+    for (int k = 0; k < m->nu; k++) ctrl[k] = a[k];
+  }
+  for (int k = 0; k < m->nu; k++) d.ctrl[k] = ctrl[k];
+  int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  for (int sstep = 0; sstep < fs; sstep++) k_step(m, &d);
+  k_make_carry(m, &d, carry);
+  int t = s.t[e] + 1;
+  s.t[e] = t;
+  if (c.task != UR3E_TASK_GYM_V2) {
+    s.ep_len[e] += 1;
+    k_store(m, s, e, &d, carry);
+    return;
+  }
+  double obs[24];
+  k_obs_v2(m, &d, obs);
+  double r = k_reward_v2(obs, a);
+  int term = k_termination_v2(m, &d, obs);
+  int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
+  double dx = obs[3] - obs[6], dy = obs[4] - obs[7], dz = obs[5] - obs[8];
+  if (sqrt(dx * dx + dy * dy + dz * dz) < 0.05) {
+    term = 1;
+    r += 50.0;
+  }
+  s.ep_return[e] += r;
+  s.ep_len[e] += 1;
+  if (rew_out) rew_out[e] = r;
+  if (term_out) term_out[e] = (unsigned char)term;
+  if (trunc_out) trunc_out[e] = (unsigned char)trunc;
+  if ((term || trunc) && c.auto_reset) {
+    if (tobs_out)
+      for (int k = 0; k < 24; k++) tobs_out[(size_t)e * 24 + k] = obs[k];
+    k_reset_env(m, c, s, e, &d, obs, carry);
+  }
+  k_store(m, s, e, &d, carry);
+  if (obs_out)
+    for (int k = 0; k < 24; k++) obs_out[(size_t)e * 24 + k] = obs[k];
+}
+
+__global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __restrict__ m, KConfig c, KState s,
+                                                      const double* __restrict__ qpos,
+                                                      const double* __restrict__ qvel,
+                                                      const double* __restrict__ warm) {
+  int e = k_env_index(c, s.n);
+  if (e < 0) return;
+  KData d;
+  for (int k = 0; k < m->nq; k++) d.qpos[k] = qpos[(size_t)e * m->nq + k];
+  for (int k = 0; k < m->nv; k++) d.qvel[k] = qvel[(size_t)e * m->nv + k];
+  for (int k = 0; k < m->nv; k++) d.qacc_warmstart[k] = warm ? warm[(size_t)e * m->nv + k] : s.warm[(size_t)k * s.n + e];
+  d.nwarn = s.nwarn[e];
+  for (int k = 0; k < m->nu; k++) d.ctrl[k] = 0;
+  k_forward(m, &d);
+  double carry[NCARRY];
+  k_make_carry(m, &d, carry);
+  k_store(m, s, e, &d, carry);
+}
+
+__global__ void k_env_get_state(int nq, int nv, KState s, double* __restrict__ qpos, double* __restrict__ qvel,
+                                double* __restrict__ warm) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  const int n = s.n;
+  if (qpos)
+    for (int k = 0; k < nq; k++) qpos[(size_t)e * nq + k] = s.qpos[(size_t)k * n + e];
+  if (qvel)
+    for (int k = 0; k < nv; k++) qvel[(size_t)e * nv + k] = s.qvel[(size_t)k * n + e];
+  if (warm)
+    for (int k = 0; k < nv; k++) warm[(size_t)e * nv + k] = s.warm[(size_t)k * n + e];
+}
+
+__global__ void k_env_get_info(KState s, int* ncon, int* ep_len, double* ep_ret, int* nwarn) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  if (ncon) ncon[e] = s.ncon[e];
+  if (ep_len) ep_len[e] = s.ep_len[e];
+  if (ep_ret) ep_ret[e] = s.ep_return[e];
+  if (nwarn) nwarn[e] = s.nwarn[e];
+}
+
+/* ================================================================== */
+/* host side: C ABI                                                    */
+/* ================================================================== */
+struct ur3e_batch {
+  int device;
+  int n;
+  ur3e_model_t host_model;
+  ur3e_model_t* d_model;
+  KConfig cfg;
+  KState st;
+  hipEvent_t ev0, ev1;
+  int timed;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t _e = (x);                                                                   \
+    if (_e != hipSuccess) return fail(UR3E_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+extern "C" int ur3e_abi_version(void) { return UR3E_ABI_VERSION; }
+extern "C" const char* ur3e_last_error(void) { return g_err.c_str(); }
+
+static int check_model(const ur3e_model_t* m) {
+  if (m->version != UR3E_MODEL_VERSION) return fail(UR3E_EMODEL, "model image version mismatch");
+  if (m->nq > K_NQ || m->nv > K_NV || m->nbody > K_NB || m->njnt > K_NJ || m->ngeom > K_NG ||
+      m->nsite > K_NS || m->nu > K_NU)
+    return fail(UR3E_EMODEL, "model exceeds kernel capacities (K_NQ/K_NV/K_NB/K_NJ/K_NG/K_NS/K_NU)");
+  if (m->ncpair > UR3E_MAXCPAIR) return fail(UR3E_EMODEL, "too many collision candidates");
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
+                                 ur3e_batch_t** out) {
+  if (!model || !cfg || !out || n_envs <= 0) return fail(UR3E_EINVAL, "null argument or n_envs <= 0");
+  int rc = check_model(model);
+  if (rc) return rc;
+  if (cfg->task < 0 || cfg->task > 3) return fail(UR3E_EINVAL, "unknown task");
+  if (cfg->task == UR3E_TASK_GYM_V2 && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
+                                        model->id_body_ghost < 0 || model->id_body_fish < 0))
+    return fail(UR3E_EMODEL, "gym ur3e-v2 task needs tcp/handle_site/ghost/fish (assets/main.xml)");
+  if ((cfg->task == UR3E_TASK_GYM_V2 || cfg->task == UR3E_TASK_TRAJ_L) && model->id_site_tcp < 0)
+    return fail(UR3E_EMODEL, "task-space control needs the tcp site");
+  if (cfg->reset_key >= model->nkey) return fail(UR3E_EINVAL, "reset_key out of range");
+  HIPCHK(hipSetDevice(device));
+  ur3e_batch* b = new ur3e_batch();
+  b->device = device;
+  b->n = n_envs;
+  b->host_model = *model;
+  b->timed = 0;
+  KConfig& c = b->cfg;
+  c.task = cfg->task;
+  c.frame_skip = cfg->frame_skip > 0 ? cfg->frame_skip : 1;
+  c.max_episode_steps = cfg->max_episode_steps;
+  c.auto_reset = cfg->auto_reset;
+  c.reset_noise = cfg->reset_noise;
+  c.reset_key = cfg->reset_key;
+  c.seed = cfg->seed;
+  c.env_id_offset = cfg->env_id_offset;
+  c.epb = cfg->envs_per_block > 0 && cfg->envs_per_block <= 64 ? cfg->envs_per_block : 16;
+  for (int k = 0; k < 12; k++) { c.gains.task[k] = cfg->task_gains[k]; c.gains.joint[k] = cfg->joint_gains[k]; }
+  KState& s = b->st;
+  s.n = n_envs;
+  size_t nd = (size_t)n_envs;
+  HIPCHK(hipMalloc(&b->d_model, sizeof(ur3e_model_t)));
+  HIPCHK(hipMemcpy(b->d_model, model, sizeof(ur3e_model_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&s.qpos, sizeof(double) * nd * model->nq));
+  HIPCHK(hipMalloc(&s.qvel, sizeof(double) * nd * model->nv));
+  HIPCHK(hipMalloc(&s.warm, sizeof(double) * nd * model->nv));
+  HIPCHK(hipMalloc(&s.carry, sizeof(double) * nd * NCARRY));
+  HIPCHK(hipMalloc(&s.t, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&s.episode, sizeof(unsigned int) * nd));
+  HIPCHK(hipMalloc(&s.ep_len, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&s.ep_return, sizeof(double) * nd));
+  HIPCHK(hipMalloc(&s.ncon, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&s.nwarn, sizeof(int) * nd));
+  HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
+  HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
+  HIPCHK(hipEventCreate(&b->ev0));
+  HIPCHK(hipEventCreate(&b->ev1));
+  /* initial reset of every env (MujocoEnv.reset at construction) */
+  int grid = (n_envs + c.epb - 1) / c.epb;
+  hipLaunchKernelGGL(k_env_reset, dim3(grid), dim3(64), 0, 0, b->d_model, c, s, nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  *out = b;
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
+  if (!b) return UR3E_OK;
+  (void)hipSetDevice(b->device);
+  void* bufs[] = {b->d_model, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn};
+  for (void* p : bufs) (void)hipFree(p);
+  (void)hipEventDestroy(b->ev0);
+  (void)hipEventDestroy(b->ev1);
+  delete b;
+  return UR3E_OK;
+}
+
+static int grid_of(const ur3e_batch* b) { return (b->n + b->cfg.epb - 1) / b->cfg.epb; }
+
+extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* d_obs, void* stream) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_reset, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg, b->st,
+                     d_mask, d_obs);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adim, double* d_obs, double* d_reward,
+                               uint8_t* d_terminated, uint8_t* d_truncated, double* d_terminal_obs, void* stream) {
+  if (!b || !d_actions) return fail(UR3E_EINVAL, "null handle or actions");
+  int need = b->cfg.task == UR3E_TASK_GYM_V2 ? 4 : (b->cfg.task == UR3E_TASK_CTRL ? b->host_model.nu : 7);
+  if (adim != need) return fail(UR3E_EINVAL, "action dimension mismatch for task (expected " + std::to_string(need) + ")");
+  HIPCHK(hipSetDevice(b->device));
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipEventRecord(b->ev0, st));
+  hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
+                     d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(b->ev1, st));
+  b->timed = 1;
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_get_state(ur3e_batch_t* b, double* d_qpos, double* d_qvel, double* d_warm, void* stream) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_get_state, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     b->host_model.nq, b->host_model.nv, b->st, d_qpos, d_qvel, d_warm);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const double* d_qvel,
+                                    const double* d_warm, void* stream) {
+  if (!b || !d_qpos || !d_qvel) return fail(UR3E_EINVAL, "null handle or state");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_set_state, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg,
+                     b->st, d_qpos, d_qvel, d_warm);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, double* d_ep_return, int* d_nwarn,
+                                   void* stream) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_get_info, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st, d_ncon,
+                     d_ep_len, d_ep_return, d_nwarn);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_num_envs(const ur3e_batch_t* b) { return b ? b->n : 0; }
+extern "C" int ur3e_batch_nq(const ur3e_batch_t* b) { return b ? b->host_model.nq : 0; }
+extern "C" int ur3e_batch_nv(const ur3e_batch_t* b) { return b ? b->host_model.nv : 0; }
+extern "C" int ur3e_batch_nu(const ur3e_batch_t* b) { return b ? b->host_model.nu : 0; }
+
+extern "C" int ur3e_batch_last_step_ms(ur3e_batch_t* b, float* ms) {
+  if (!b || !ms) return fail(UR3E_EINVAL, "null argument");
+  if (!b->timed) return fail(UR3E_EINVAL, "no step recorded");
+  HIPCHK(hipEventSynchronize(b->ev1));
+  HIPCHK(hipEventElapsedTime(ms, b->ev0, b->ev1));
+  return UR3E_OK;
+}

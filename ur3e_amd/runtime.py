@@ -1,0 +1,194 @@
+"""Host-side binding of the MI355X C ABI (include/ur3e_batch.h).
+
+`Batch` owns one `ur3e_batch_t` handle: N environments resident in HBM on one
+GPU.  Buffers exchanged with the library are torch tensors on that device; all
+calls enqueue on torch's current stream, so torch events time them and torch
+ops consume the results without host round-trips.
+
+There is no CPU fallback: if the HIP library or a GPU is missing this module
+raises.  (The CPU oracle in oracle/ is test infrastructure and is never used
+here.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .model.compiler import UR3eModelC, load_json, to_ctypes
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libur3e_amd.so")
+ASSETS = os.path.join(_HERE, "assets")
+
+TASK_GYM_V2, TASK_TRAJ_L, TASK_MOVE_J, TASK_CTRL = 0, 1, 2, 3
+
+# controller/config/config_l_mug.yml (used by UR3eEnv2, ur3e_env2.py:66-68)
+GAINS_L_MUG = dict(kp_pos=[220.0, 220.0, 120.0], kd_pos=[20.0, 20.0, 40.0],
+                   kp_rot=[35.0, 15.0, 15.0], kd_rot=[2.0, 2.0, 2.0])
+# controller/config/config_j.yml (move_j)
+GAINS_J = dict(kp=[20.0, 380.0, 300.0, 20.0, 30.0, 10.0], kd=[5.0] * 6)
+
+_lib = None
+
+
+class ConfigC(ctypes.Structure):
+    _fields_ = [
+        ("task", ctypes.c_int), ("frame_skip", ctypes.c_int), ("max_episode_steps", ctypes.c_int),
+        ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
+        ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
+        ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
+    ]
+
+
+def load_library():
+    """Load the in-tree HIP library; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"MI355X library missing: {LIB_PATH} (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    L.ur3e_last_error.restype = ctypes.c_char_p
+    L.ur3e_batch_create.argtypes = [vp, vp, ip, ip, ctypes.POINTER(vp)]
+    L.ur3e_batch_destroy.argtypes = [vp]
+    L.ur3e_batch_reset.argtypes = [vp, vp, vp, vp]
+    L.ur3e_batch_step.argtypes = [vp, vp, ip, vp, vp, vp, vp, vp, vp]
+    L.ur3e_batch_get_state.argtypes = [vp, vp, vp, vp, vp]
+    L.ur3e_batch_set_state.argtypes = [vp, vp, vp, vp, vp]
+    L.ur3e_batch_get_info.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.ur3e_batch_last_step_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu"):
+        getattr(L, f).argtypes = [vp]
+    _lib = L
+    del dp
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"ur3e library error {rc}: {_lib.ur3e_last_error().decode()}")
+
+
+def load_model(name: str = "main"):
+    """Compiled model dict + C image for one of the reference models (main, ur3e_2f85, ur3e_raw)."""
+    md = load_json(os.path.join(ASSETS, f"{name}.model.json"))
+    return md, to_ctypes(md)
+
+
+def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
+                reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
+                task_gains=None, joint_gains=None) -> ConfigC:
+    c = ConfigC()
+    c.task = task
+    c.frame_skip = frame_skip
+    c.max_episode_steps = max_episode_steps
+    c.auto_reset = int(auto_reset)
+    c.reset_noise = int(reset_noise)
+    if reset_key is None:
+        reset_key = model["id_key_down"] if model is not None else -1
+    c.reset_key = reset_key
+    tg = task_gains or GAINS_L_MUG
+    g = list(tg["kp_pos"]) + list(tg["kd_pos"]) + list(tg["kp_rot"]) + list(tg["kd_rot"])
+    jg = joint_gains or GAINS_J
+    j = list(jg["kp"]) + list(jg["kd"])
+    for k in range(12):
+        c.task_gains[k] = g[k]
+        c.joint_gains[k] = j[k]
+    c.seed = seed
+    c.env_id_offset = env_id_offset
+    c.envs_per_block = envs_per_block
+    return c
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Batch:
+    """N UR3e environments on one GPU (C ABI handle + device tensors)."""
+
+    def __init__(self, model_c: UR3eModelC, cfg: ConfigC, n_envs: int, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("ur3e_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.torch = torch
+        self.L = load_library()
+        self.device = torch.device("cuda", device)
+        self.model_c = model_c
+        self.cfg = cfg
+        self.n = n_envs
+        self.nq, self.nv, self.nu = model_c.nq, model_c.nv, model_c.nu
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(self.device)
+        _check(self.L.ur3e_batch_create(ctypes.byref(model_c), ctypes.byref(cfg), n_envs, device, ctypes.byref(h)))
+        self.h = h
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.obs = torch.zeros((n_envs, 24), **f64)
+        self.reward = torch.zeros(n_envs, **f64)
+        self.terminated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
+        self.truncated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
+        self.terminal_obs = torch.zeros((n_envs, 24), **f64)
+
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ur3e_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, mask=None):
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
+        _check(self.L.ur3e_batch_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()))
+        return self.obs
+
+    def step(self, actions):
+        a = actions.to(device=self.device, dtype=self.torch.float64).contiguous()
+        _check(self.L.ur3e_batch_step(self.h, _ptr(a), a.shape[1], _ptr(self.obs), _ptr(self.reward),
+                                      _ptr(self.terminated), _ptr(self.truncated), _ptr(self.terminal_obs),
+                                      self._stream()))
+        return self.obs, self.reward, self.terminated, self.truncated, self.terminal_obs
+
+    def get_state(self):
+        t = self.torch
+        qp = t.empty((self.n, self.nq), dtype=t.float64, device=self.device)
+        qv = t.empty((self.n, self.nv), dtype=t.float64, device=self.device)
+        wa = t.empty((self.n, self.nv), dtype=t.float64, device=self.device)
+        _check(self.L.ur3e_batch_get_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
+        return qp, qv, wa
+
+    def set_state(self, qpos, qvel, warm=None):
+        t = self.torch
+        qp = t.as_tensor(qpos, dtype=t.float64).to(self.device).contiguous()
+        qv = t.as_tensor(qvel, dtype=t.float64).to(self.device).contiguous()
+        wa = None if warm is None else t.as_tensor(warm, dtype=t.float64).to(self.device).contiguous()
+        _check(self.L.ur3e_batch_set_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
+
+    def get_info(self):
+        t = self.torch
+        nc = t.empty(self.n, dtype=t.int32, device=self.device)
+        el = t.empty(self.n, dtype=t.int32, device=self.device)
+        er = t.empty(self.n, dtype=t.float64, device=self.device)
+        nw = t.empty(self.n, dtype=t.int32, device=self.device)
+        _check(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
+        return dict(ncon=nc, ep_len=el, ep_return=er, nwarn=nw)
+
+    def last_step_ms(self) -> float:
+        ms = ctypes.c_float()
+        _check(self.L.ur3e_batch_last_step_ms(self.h, ctypes.byref(ms)))
+        return ms.value
+
+
+__all__ = ["Batch", "make_config", "load_model", "load_library", "TASK_GYM_V2", "TASK_TRAJ_L", "TASK_MOVE_J",
+           "TASK_CTRL", "GAINS_L_MUG", "GAINS_J", "np"]
