@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 ALGO_BYTES_PER_ENV_STEP = 1898
 
 
-def cpu_baseline(n_envs_sample=128, steps=20, seed=0):
+def cpu_baseline(n_envs_sample=4096, steps=100, seed=0):
     """Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of the same workload."""
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
@@ -68,8 +68,8 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--envs-per-block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-envs", type=int, default=128)
-    ap.add_argument("--cpu-sample-steps", type=int, default=20)
+    ap.add_argument("--cpu-sample-envs", type=int, default=4096)
+    ap.add_argument("--cpu-sample-steps", type=int, default=100)
     ap.add_argument("--no-gather", action="store_true")
     args = ap.parse_args()
 

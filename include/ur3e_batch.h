@@ -73,6 +73,7 @@ typedef struct ur3e_batch ur3e_batch_t;
 int ur3e_abi_version(void);
 const char* ur3e_last_error(void);
 
+/* allocates N envs at qpos0 / zero velocity; like gymnasium, call ur3e_batch_reset before stepping */
 int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
                       ur3e_batch_t** out);
 int ur3e_batch_destroy(ur3e_batch_t* b);

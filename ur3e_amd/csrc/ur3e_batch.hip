@@ -456,6 +456,17 @@ __global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __rest
   k_store(m, s, e, &d, carry);
 }
 
+/* create(): qpos0 / zero velocities, episode 0; envs are valid after ur3e_batch_reset */
+__global__ void k_env_init(const ur3e_model_t* __restrict__ m, KState s) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  const int n = s.n;
+  for (int k = 0; k < m->nq; k++) s.qpos[(size_t)k * n + e] = m->qpos0[k];
+  for (int k = 0; k < m->nv; k++) { s.qvel[(size_t)k * n + e] = 0; s.warm[(size_t)k * n + e] = 0; }
+  for (int k = 0; k < NCARRY; k++) s.carry[(size_t)k * n + e] = 0;
+  s.t[e] = 0; s.episode[e] = 0; s.ep_len[e] = 0; s.ep_return[e] = 0; s.ncon[e] = 0; s.nwarn[e] = 0;
+}
+
 __global__ void k_env_get_state(int nq, int nv, KState s, double* __restrict__ qpos, double* __restrict__ qvel,
                                 double* __restrict__ warm) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -565,9 +576,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
-  /* initial reset of every env (MujocoEnv.reset at construction) */
-  int grid = (n_envs + c.epb - 1) / c.epb;
-  hipLaunchKernelGGL(k_env_reset, dim3(grid), dim3(64), 0, 0, b->d_model, c, s, nullptr, nullptr);
+  /* qpos0 / zero state; like a gymnasium Env, call ur3e_batch_reset before the first step */
+  hipLaunchKernelGGL(k_env_init, dim3((n_envs + 255) / 256), dim3(256), 0, 0, b->d_model, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   *out = b;

@@ -131,6 +131,7 @@ class Batch:
         self.terminated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
         self.truncated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
         self.terminal_obs = torch.zeros((n_envs, 24), **f64)
+        self.reset()
 
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
