@@ -175,3 +175,36 @@ void ur3o_forward_state(const ur3e_model_t* m, const double* qpos, const double*
   if (ncon) *ncon = d->ncon;
   free(d);
 }
+
+/* predicates on a synthetic contact list (golden tests of gym_utils.py:98-172, ur3e_env2.py:230-254) */
+void ur3o_predicates(const ur3e_model_t* m, int ncon, const int* geom1, const int* geom2, const double* tcp,
+                     const double* hnd, const double* obs, int* out) {
+  ur3o_data* d = (ur3o_data*)calloc(1, sizeof(ur3o_data));
+  d->ncon = ncon;
+  for (int k = 0; k < ncon; k++) { d->contact[k].geom1 = geom1[k]; d->contact[k].geom2 = geom2[k]; }
+  for (int k = 0; k < 3; k++) {
+    d->site_xpos[m->id_site_tcp][k] = tcp[k];
+    d->site_xpos[m->id_site_handle][k] = hnd[k];
+  }
+  double o[24];
+  ur3o_obs_v2(m, d, o); /* obs[23] = robust grasp state (velocities are zero here) */
+  out[0] = ur3o_block_grasp_state(m, d);
+  out[1] = (int)o[23];
+  out[2] = ur3o_self_collision(m, d);
+  out[3] = hnd[2] <= m->fish_topple_z;
+  out[4] = ur3o_termination_v2(m, d, obs);
+  free(d);
+}
+
+/* deterministic-math probe for tests: fn 0 sin, 1 cos, 2 exp, 3 tanh, 4 atan, 5 atan2 */
+#include "../ur3e_amd/csrc/detmath.h"
+double ur3o_detmath(int fn, double x, double y) {
+  switch (fn) {
+    case 0: return ur3e_sin(x);
+    case 1: return ur3e_cos(x);
+    case 2: return ur3e_exp(x);
+    case 3: return ur3e_tanh(x);
+    case 4: return ur3e_atan(x);
+    default: return ur3e_atan2(x, y);
+  }
+}

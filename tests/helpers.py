@@ -1,0 +1,43 @@
+"""Test helpers: an oracle-backed CPU stepper with the runtime.Batch interface
+(torch CPU tensors), used to test host logic (VecEnv, sharding) without a GPU.
+Test infrastructure only."""
+import numpy as np
+
+
+def oracle_config(po, c):
+    oc = po.OracleConfig()
+    for f, _ in po.OracleConfig._fields_:
+        v = getattr(c, f)
+        if f in ("task_gains", "joint_gains"):
+            for k in range(12):
+                getattr(oc, f)[k] = v[k]
+        else:
+            setattr(oc, f, v)
+    return oc
+
+
+class OracleStepper:
+    def __init__(self, n, seed=0, env_id_offset=0, max_episode_steps=2500, model="main"):
+        import torch
+        from oracle import pyoracle as po
+        from ur3e_amd import runtime as rt
+        self.torch = torch
+        md, mc = rt.load_model(model)
+        cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=max_episode_steps, model=md,
+                             seed=seed, env_id_offset=env_id_offset)
+        self.cfg = cfg
+        self.ob = po.OracleBatch(mc, oracle_config(po, cfg), n)
+        self.n = n
+        self.obs = torch.from_numpy(self.ob.obs.copy())
+
+    def reset(self):
+        return self.torch.from_numpy(self.ob.obs.copy())
+
+    def step(self, actions):
+        a = actions.detach().cpu().numpy() if hasattr(actions, "detach") else np.asarray(actions)
+        obs, rew, term, trunc, tobs = self.ob.step(a)
+        t = self.torch
+        return (t.from_numpy(obs), t.from_numpy(rew), t.from_numpy(term), t.from_numpy(trunc), t.from_numpy(tobs))
+
+    def close(self):
+        pass

@@ -1,0 +1,35 @@
+"""Task predicates (gym_utils.py:98-172, ur3e_env2.py:230-254) of the oracle vs
+golden vectors from the reference run on synthetic contact lists."""
+import ctypes
+
+import numpy as np
+
+from oracle import pyoracle as po
+
+
+def test_collision_cache_sets(golden, main_model):
+    md, _ = main_model
+    arm = [b for b in range(md["nbody"]) if (md["mask_arm_bodies"] >> b) & 1]
+    grip = [b for b in range(md["nbody"]) if (md["mask_gripper_bodies"] >> b) & 1]
+    assert arm == list(golden["cache_arm"])
+    assert grip == list(golden["cache_gripper"])
+
+
+def test_predicates(golden, main_model):
+    md, mc = main_model
+    L = po.lib()
+    for i in range(len(golden["pred_ncon"])):
+        nc = int(golden["pred_ncon"][i])
+        pairs = golden["pred_pairs"][i][:nc]
+        g1 = np.ascontiguousarray(pairs[:, 0], dtype=np.int32)
+        g2 = np.ascontiguousarray(pairs[:, 1], dtype=np.int32)
+        out = np.zeros(5, np.int32)
+        args = [np.ascontiguousarray(golden[k][i], dtype=np.float64) for k in ("pred_tcp", "pred_hnd", "pred_obs")]
+        L.ur3o_predicates(ctypes.byref(mc), ctypes.c_int(nc), g1.ctypes.data_as(ctypes.c_void_p),
+                          g2.ctypes.data_as(ctypes.c_void_p), *[a.ctypes.data_as(ctypes.c_void_p) for a in args],
+                          out.ctypes.data_as(ctypes.c_void_p))
+        assert out[0] == golden["pred_grasp"][i], i
+        assert out[1] == golden["pred_robust"][i], i
+        assert out[2] == golden["pred_selfcol"][i], i
+        assert out[3] == golden["pred_toppled"][i], i
+        assert out[4] == golden["pred_term"][i], i

@@ -1,0 +1,113 @@
+"""Trajectory builders (host side), restating controller/build_traj.py.
+
+* build_traj_l_point_custom  (build_traj.py:215-254): 15-point linear segment
+  (t[1:] of linspace(0, 1, 16)), each row held `hold` times.
+* build_traj_l_pick_place    (build_traj.py:28-59): pick / up (+0.15 z, grip
+  1 - g) / place (+0.025 z) / drop (grip 0); hold is hard-coded 120 (quirk:
+  the `hold` argument is ignored).  Unlike the
+  reference, `destinations` are not mutated in place.
+* build_traj_j               (build_traj.py:387-470): np.random.seed(42) control
+  points + cubic interp1d, 500 samples, held `hold` times, grip 0.
+
+Also a torch version of pick_place that evaluates rows analytically per env
+and step on the GPU (`PickPlaceTorch`), used by the batched scripted driver
+(controller/move_l_mug.py:67-81 semantics) without materialising [7200, 7]
+per env.  Pinned against the reference by tests/golden (bit-exact).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+HOLD_PICK_PLACE = 120
+NUM_POINTS = 15
+
+
+def _linear_rows(start, stop, num_points=NUM_POINTS):
+    """scipy interp1d(kind='linear') on t_control=[0, 1] at linspace(0,1,n+1)[1:].
+
+    scipy 1.15 routes 1-D linear interp1d to np.interp: slope*(x - x0) + y0,
+    and x == x[-1] returns y[-1] exactly (so each segment ends exactly on `stop`)."""
+    t = np.linspace(0, 1, num_points + 1)[1:]
+    start = np.asarray(start, dtype=np.float64)
+    stop = np.asarray(stop, dtype=np.float64)
+    slope = (stop - start) / (1.0 - 0.0)
+    rows = slope[None, :] * (t[:, None] - 0.0) + start[None, :]
+    rows[-1] = stop
+    return rows
+
+
+def build_traj_l_point_custom(start, stop, hold, num_points=NUM_POINTS):
+    return np.repeat(_linear_rows(start, stop, num_points), repeats=hold, axis=0)
+
+
+def pick_place_waypoints(start, pick, place):
+    """The 4 segment endpoint pairs (A, B) of build_traj_l_pick_place."""
+    start = np.asarray(start, dtype=np.float64)
+    pick = np.asarray(pick, dtype=np.float64)
+    place = np.asarray(place, dtype=np.float64) + np.array([0, 0, 0.025, 0, 0, 0, 0])
+    end_pick = _linear_rows(start, pick)[-1]
+    up = end_pick + np.array([0, 0, 0.15, 0, 0, 0, 1 - end_pick[-1]])
+    end_up = _linear_rows(end_pick, up)[-1]
+    end_place = _linear_rows(end_up, place)[-1]
+    drop = np.append(end_place[:-1], 0.0)
+    return [(start, pick), (end_pick, up), (end_up, place), (end_place, drop)]
+
+
+def build_traj_l_pick_place(start, destinations, hold=HOLD_PICK_PLACE):
+    pick, place = destinations
+    segs = pick_place_waypoints(start, pick, place)
+    return np.vstack([build_traj_l_point_custom(a, b, HOLD_PICK_PLACE) for a, b in segs])
+
+
+def build_traj_j(start, hold):
+    from scipy.interpolate import interp1d
+    num_points = 500
+    t = np.linspace(0, 1, num_points)
+    rs = np.random.RandomState(42)  # same MT19937 stream as np.random.seed(42)
+    bounds = [[0.2, 0.5], [-0.3, 0.3], [0.4, 0.8], [0.4, 0.8], [0.4, 0.8], [0.4, 0.8]]
+    ncp = 10
+    t_control = np.linspace(0, 1, ncp + 1)
+    cols = []
+    for j in range(6):
+        ctrl = np.concatenate([np.asarray(start, dtype=np.float64)[j:j + 1],
+                               rs.uniform(bounds[j][0], bounds[j][1], ncp)])
+        cols.append(interp1d(t_control, ctrl, kind="cubic")(t))
+    g = np.tile([0, 0, 0], num_points // 3 + 1)[:num_points]
+    return np.repeat(np.vstack(cols + [g]).T, repeats=hold, axis=0)
+
+
+class PickPlaceTorch:
+    """Per-env build_traj_l_pick_place rows evaluated on the GPU: row(t) for all envs.
+
+    starts/picks/places: [N, 7] float64 tensors.  Row t (0 <= t < 7200) equals
+    build_traj_l_pick_place(start_i, [pick_i, place_i])[t] bit-for-bit.
+    """
+
+    def __init__(self, starts, picks, places):
+        import torch
+        self.torch = torch
+        dev = starts.device
+        dz = torch.tensor([0, 0, 0.025, 0, 0, 0, 0], dtype=torch.float64, device=dev)
+        self.t = torch.from_numpy(np.linspace(0, 1, NUM_POINTS + 1)).to(dev)
+        places = places + dz
+        # np.interp returns the segment end exactly at t == 1
+        end_pick = picks
+        up = end_pick.clone()
+        up[:, 2] = end_pick[:, 2] + 0.15
+        up[:, 6] = end_pick[:, 6] + (1 - end_pick[:, 6])
+        end_up = up
+        end_place = places
+        drop = end_place.clone()
+        drop[:, 6] = 0.0
+        self.A = torch.stack([starts, end_pick, end_up, end_place])  # [4, N, 7]
+        self.B = torch.stack([picks, up, places, drop])
+        self.T = 4 * NUM_POINTS * HOLD_PICK_PLACE
+
+    def row(self, t: int):
+        seg = t // (NUM_POINTS * HOLD_PICK_PLACE)
+        k = (t % (NUM_POINTS * HOLD_PICK_PLACE)) // HOLD_PICK_PLACE
+        a, b = self.A[seg], self.B[seg]
+        if k + 1 == NUM_POINTS:
+            return b.clone()
+        slope = (b - a) / (1.0 - 0.0)
+        return slope * (self.t[k + 1] - 0.0) + a

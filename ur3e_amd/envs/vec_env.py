@@ -1,0 +1,123 @@
+"""Stable-Baselines3-compatible batched VecEnv over N GPU-resident UR3e envs.
+
+Replaces `make_vec_env("gymnasium_env/ur3e-v2", n_envs, vec_env_cls=SubprocVecEnv)`
+(gymnasium_src/scripts/regular_rl/rl/train_rl.py:38-44): instead of N worker
+processes each owning a MuJoCo env and talking over pipes, all N envs live in
+HBM and one fused kernel launch steps them all.
+
+API (SB3 VecEnv): num_envs, observation_space, action_space, reset(),
+step_async(actions), step_wait() -> (obs, rewards, dones, infos), step(),
+close(), get_attr/set_attr/env_method/env_is_wrapped, seed().  infos[i] carries
+"terminal_observation" and "TimeLimit.truncated" on episode end (SB3
+auto-reset semantics) and "episode" = {r, l, t} like SB3's Monitor wrapper.
+`step_torch()` returns device tensors for a torch-ROCm policy (no host copy).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .spaces import Box
+from .ur3e_env2 import UR3E_V2_ACTION_HIGH, UR3E_V2_ACTION_LOW
+
+try:  # subclass SB3's VecEnv when it is installed (it is not in this image)
+    from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _SB3VecEnv
+except Exception:  # pragma: no cover
+    _SB3VecEnv = object
+
+
+class UR3eVecEnv(_SB3VecEnv):
+    def __init__(self, num_envs: int = 4096, device: int = 0, seed: int = 0, stepper=None, env_id_offset: int = 0,
+                 envs_per_block: int = 0, max_episode_steps: int = 2500):
+        self.num_envs = num_envs
+        self.observation_space = Box(low=-np.inf, high=np.inf, shape=(24,), dtype=np.float64)
+        self.action_space = Box(low=UR3E_V2_ACTION_LOW, high=UR3E_V2_ACTION_HIGH, dtype=np.float64)
+        self.render_mode = None
+        if stepper is None:
+            from .. import runtime as rt
+            md, mc = rt.load_model("main")
+            cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=max_episode_steps,
+                                 model=md, seed=seed, env_id_offset=env_id_offset, envs_per_block=envs_per_block)
+            stepper = rt.Batch(mc, cfg, num_envs, device=device)
+        self.stepper = stepper
+        self._actions = None
+        self._ep_ret = np.zeros(num_envs)
+        self._ep_len = np.zeros(num_envs, dtype=np.int64)
+        self._t0 = time.time()
+        self._attrs = {}
+
+    # -- SB3 VecEnv interface ------------------------------------------------
+    def reset(self):
+        obs = self.stepper.reset()
+        self._ep_ret[:] = 0
+        self._ep_len[:] = 0
+        return _np(obs)
+
+    def step_async(self, actions):
+        self._actions = actions
+
+    def step_wait(self):
+        obs, rew, term, trunc, tobs = self.step_torch(self._actions)
+        obs, rew, term, trunc = _np(obs), _np(rew), _np(term).astype(bool), _np(trunc).astype(bool)
+        dones = term | trunc
+        self._ep_ret += rew
+        self._ep_len += 1
+        infos = [{} for _ in range(self.num_envs)]
+        if dones.any():
+            tobs = _np(tobs)
+            now = round(time.time() - self._t0, 6)
+            for i in np.flatnonzero(dones):
+                infos[i]["terminal_observation"] = tobs[i].copy()
+                infos[i]["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
+                infos[i]["episode"] = {"r": float(self._ep_ret[i]), "l": int(self._ep_len[i]), "t": now}
+                self._ep_ret[i] = 0
+                self._ep_len[i] = 0
+        return obs, rew, dones, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def step_torch(self, actions):
+        """Device-tensor step: returns (obs, reward, terminated, truncated, terminal_obs) on the GPU."""
+        import torch
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, dtype=np.float64))
+        # no clipping here: like UR3eEnv2.step, actions are used as given (SB3 clips to the Box itself)
+        return self.stepper.step(a.reshape(self.num_envs, 4).to(torch.float64))
+
+    def close(self):
+        if hasattr(self.stepper, "close"):
+            self.stepper.close()
+
+    def seed(self, seed=None):
+        return [seed] * self.num_envs
+
+    def get_attr(self, attr_name, indices=None):
+        n = len(self._indices(indices))
+        return [self._attrs.get(attr_name, getattr(self, attr_name, None))] * n
+
+    def set_attr(self, attr_name, value, indices=None):
+        self._attrs[attr_name] = value
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return [None] * len(self._indices(indices))
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False] * len(self._indices(indices))
+
+    def get_images(self):
+        return [None] * self.num_envs
+
+    def _indices(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+
+def _np(x):
+    if hasattr(x, "detach"):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
