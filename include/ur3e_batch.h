@@ -65,7 +65,9 @@ typedef struct ur3e_config_t {
   double joint_gains[12];/* kp[6], kd[6] (config_j.yml) */
   unsigned long long seed; /* Philox key for reset noise */
   int env_id_offset;     /* global id of local env 0 (multi-GPU shards) */
-  int envs_per_block;    /* lanes used per 64-wide wavefront (1..64; 0 = auto) */
+  int envs_per_block;    /* kernel layout: 0 (default) = one 128-lane workgroup per env, working set in
+                            LDS (v2); -64 = one 64-lane wavefront per env (v2); 1..64 = one env per
+                            lane with that many envs per wavefront (v1, lane-private scratch) */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;

@@ -37,8 +37,9 @@ extern "C" {
 #define UR3E_MAXTOUCH 4
 
 /* per-env dynamic capacities (the kernels size scratch from these) */
-#define UR3E_MAXCON 48                                   /* contacts per env (main.xml: nconmax 100) */
-#define UR3E_MAXEFC (3 * UR3E_MAXCON + 40)               /* constraint rows per env */
+#define UR3E_MAXCON 40                                   /* contacts per env (main.xml: nconmax 100) */
+#define UR3E_MAXEFC (3 * UR3E_MAXCON + 40)               /* constraint rows per env; groups (connect,
+                                                            contact) are reserved whole, first overflow stops */
 
 /* joint types (MuJoCo numbering) */
 #define UR3E_JNT_FREE 0

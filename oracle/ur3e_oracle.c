@@ -382,8 +382,13 @@ static void solve_tree(const ur3e_model_t* m, const double A[UR3E_MAXNV][UR3E_MA
   for (int i = nv - 1; i >= 0; i--)
     for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) x[j] -= A[i][j] * x[i];
   for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
-  for (int i = 0; i < nv; i++)
-    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) x[i] -= A[i][j] * x[j];
+  /* forward pass: ancestors farthest-first (increasing index), so the GPU can run it as a
+     column sweep with the same per-element operation order */
+  for (int i = 0; i < nv; i++) {
+    int anc[UR3E_MAXNV], na = 0;
+    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) anc[na++] = j;
+    for (int t = na - 1; t >= 0; t--) x[i] -= A[i][anc[t]] * x[anc[t]];
+  }
 }
 
 static void mul_M(const ur3e_model_t* m, const ur3o_data* d, double* r, const double* v) {
@@ -720,6 +725,7 @@ static void make_constraint(const ur3e_model_t* m, ur3o_data* d) {
       jac_point(m, d, b1, p1, jp1, 0);
       jac_point(m, d, b2, p2, jp2, 0);
       double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      if (d->nefc + 3 > UR3E_MAXEFC) { d->efc_overflow = 1; return; }
       for (int k = 0; k < 3; k++) {
         int r = add_row(d, UR3O_CNSTR_EQUALITY, e, p1[k] - p2[k], 0, 0, diag);
         if (r < 0) return;
@@ -781,6 +787,7 @@ static void make_constraint(const ur3e_model_t* m, ur3o_data* d) {
     jac_point(m, d, b1, c->pos, jp1, 0);
     jac_point(m, d, b2, c->pos, jp2, 0);
     double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    if (d->nefc + 3 > UR3E_MAXEFC) { d->efc_overflow = 1; return; }
     c->efc_address = d->nefc;
     for (int k = 0; k < 3; k++) {
       int r = add_row(d, UR3O_CNSTR_CONTACT_ELLIPTIC, ci, c->dist, c->includemargin, 0, diag);
@@ -1192,7 +1199,7 @@ static void hessian_solve(const solver_ctx* s, double* x, const double* b) {
   }
   for (int i = nv - 1; i >= 0; i--) {
     double v = x[i];
-    for (int k = i + 1; k < nv; k++) v -= s->H[k][i] * x[k];
+    for (int k = nv - 1; k > i; k--) v -= s->H[k][i] * x[k];
     x[i] = v / s->H[i][i];
   }
 }

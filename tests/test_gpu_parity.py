@@ -29,7 +29,7 @@ def _oracle_cfg(po, c):
     return oc
 
 
-def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=16, check_every=1):
+def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1):
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
@@ -74,8 +74,11 @@ def _gym_actions(rng, n, md):
     return rng.uniform(lo, hi, size=(n, 4))
 
 
-def test_gym_v2_random_actions_short():
-    _run_pair("main", 0, 64, 60, _gym_actions)
+# kernel layouts: 0 = workgroup-per-env (128 lanes, default), -64 = one wavefront per env,
+# 16 = one env per lane (16 envs per wavefront, v1)
+@pytest.mark.parametrize("epb", [0, -64, 16])
+def test_gym_v2_random_actions_short(epb):
+    _run_pair("main", 0, 64, 60, _gym_actions, epb=epb)
 
 
 def test_gym_v2_grasp_region():

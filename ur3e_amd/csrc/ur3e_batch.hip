@@ -30,6 +30,7 @@
 
 #include "../../include/ur3e_batch.h"
 #include "ur3e_engine.h"
+#include "ur3e_wave.h"
 
 #define NCARRY 54
 
@@ -281,10 +282,14 @@ KD double k_uniform01(unsigned long long seed, unsigned int env_id, unsigned int
 /* ================================================================== */
 struct KState {
   int n;
-  double* qpos;   /* [nq][n] */
-  double* qvel;   /* [nv][n] */
-  double* warm;   /* [nv][n] */
-  double* carry;  /* [NCARRY][n] */
+  /* element (field k, env e) at k*fs + e*es: lane-per-env mode uses [field][env] (fs = n, es = 1),
+     workgroup-per-env mode uses [env][field] (fs = 1, es = width) so a workgroup's loads coalesce */
+  int fs;
+  int es_q, es_v, es_c;
+  double* qpos;   /* nq fields */
+  double* qvel;   /* nv fields */
+  double* warm;   /* nv fields */
+  double* carry;  /* NCARRY fields */
   int* t;
   unsigned int* episode;
   int* ep_len;
@@ -301,20 +306,22 @@ struct KConfig {
   KGains gains;
 };
 
+KD size_t SQ(const KState& s, int k, int e) { return (size_t)k * s.fs + (size_t)e * s.es_q; }
+KD size_t SV(const KState& s, int k, int e) { return (size_t)k * s.fs + (size_t)e * s.es_v; }
+KD size_t SC(const KState& s, int k, int e) { return (size_t)k * s.fs + (size_t)e * s.es_c; }
+
 KD void k_load(KModel m, const KState& s, int e, KData* d) {
-  const int n = s.n;
-  for (int k = 0; k < m->nq; k++) d->qpos[k] = s.qpos[(size_t)k * n + e];
-  for (int k = 0; k < m->nv; k++) d->qvel[k] = s.qvel[(size_t)k * n + e];
-  for (int k = 0; k < m->nv; k++) d->qacc_warmstart[k] = s.warm[(size_t)k * n + e];
+  for (int k = 0; k < m->nq; k++) d->qpos[k] = s.qpos[SQ(s, k, e)];
+  for (int k = 0; k < m->nv; k++) d->qvel[k] = s.qvel[SV(s, k, e)];
+  for (int k = 0; k < m->nv; k++) d->qacc_warmstart[k] = s.warm[SV(s, k, e)];
   d->nwarn = s.nwarn[e];
 }
 
 KD void k_store(KModel m, const KState& s, int e, const KData* d, const double* carry) {
-  const int n = s.n;
-  for (int k = 0; k < m->nq; k++) s.qpos[(size_t)k * n + e] = d->qpos[k];
-  for (int k = 0; k < m->nv; k++) s.qvel[(size_t)k * n + e] = d->qvel[k];
-  for (int k = 0; k < m->nv; k++) s.warm[(size_t)k * n + e] = d->qacc_warmstart[k];
-  for (int k = 0; k < NCARRY; k++) s.carry[(size_t)k * n + e] = carry[k];
+  for (int k = 0; k < m->nq; k++) s.qpos[SQ(s, k, e)] = d->qpos[k];
+  for (int k = 0; k < m->nv; k++) s.qvel[SV(s, k, e)] = d->qvel[k];
+  for (int k = 0; k < m->nv; k++) s.warm[SV(s, k, e)] = d->qacc_warmstart[k];
+  for (int k = 0; k < NCARRY; k++) s.carry[SC(s, k, e)] = carry[k];
   s.ncon[e] = d->ncon;
   s.nwarn[e] = d->nwarn;
 }
@@ -384,7 +391,7 @@ __global__ __launch_bounds__(64) void k_env_step(const ur3e_model_t* __restrict_
   double ctrl[K_NU];
   double carry[NCARRY];
   if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
-    for (int k = 0; k < NCARRY; k++) carry[k] = s.carry[(size_t)k * n + e];
+    for (int k = 0; k < NCARRY; k++) carry[k] = s.carry[SC(s, k, e)];
     double traj[7];
     if (c.task == UR3E_TASK_GYM_V2) {
       traj[0] = a[0]; traj[1] = a[1]; traj[2] = a[2];
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __rest
   KData d;
   for (int k = 0; k < m->nq; k++) d.qpos[k] = qpos[(size_t)e * m->nq + k];
   for (int k = 0; k < m->nv; k++) d.qvel[k] = qvel[(size_t)e * m->nv + k];
-  for (int k = 0; k < m->nv; k++) d.qacc_warmstart[k] = warm ? warm[(size_t)e * m->nv + k] : s.warm[(size_t)k * s.n + e];
+  for (int k = 0; k < m->nv; k++) d.qacc_warmstart[k] = warm ? warm[(size_t)e * m->nv + k] : s.warm[SV(s, k, e)];
   d.nwarn = s.nwarn[e];
   for (int k = 0; k < m->nu; k++) d.ctrl[k] = 0;
   k_forward(m, &d);
@@ -456,14 +463,300 @@ __global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __rest
   k_store(m, s, e, &d, carry);
 }
 
+
+/* ================================================================== */
+/* workgroup-per-env kernels (v2, default): see ur3e_wave.h            */
+/* ================================================================== */
+/* carry from the LDS working set: tcp pose, arm Jacobian (6x6), qfrc_bias[0:6] */
+template <int NT>
+__device__ static void w_make_carry(KModel m, const KPlan* __restrict__ pl, const KS& s, double* carry) {
+  const int tid = threadIdx.x;
+  int st = m->id_site_tcp;
+  if (st < 0) {
+    for (int k = tid; k < NCARRY; k += NT) carry[k] = 0;
+    return;
+  }
+  int b = m->site_bodyid[st];
+  const double* c = s.subtree_com[m->body_rootid[b]];
+  const double* p = s.site_xpos[st];
+  double off[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+  for (int k = tid; k < NCARRY; k += NT) {
+    double v;
+    if (k < 3) {
+      v = p[k];
+    } else if (k < 12) {
+      v = s.site_xmat[st][k - 3];
+    } else if (k < 48) {
+      int r = (k - 12) / 6, col = (k - 12) % 6;
+      if (r < 3) {
+        double jp[3];
+        w_jacp_col(m, pl, s, b, off, col, jp);
+        v = jp[r];
+      } else {
+        v = ((pl->body_dof_mask[b] >> col) & 1u) ? s.cdof[col][r - 3] : 0.0;
+      }
+    } else {
+      v = s.qfrc_bias[k - 48];
+    }
+    carry[k] = v;
+  }
+}
+
+KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
+  int b = m->site_bodyid[site];
+  const double* cv = s.cvel[b];
+  const double* c = s.subtree_com[m->body_rootid[b]];
+  double dif[3] = {s.site_xpos[site][0] - c[0], s.site_xpos[site][1] - c[1], s.site_xpos[site][2] - c[2]};
+  double cr[3];
+  k_cross3(cr, dif, cv);
+  res[0] = cv[0]; res[1] = cv[1]; res[2] = cv[2];
+  res[3] = cv[3] - cr[0]; res[4] = cv[4] - cr[1]; res[5] = cv[5] - cr[2];
+}
+
+/* UR3eEnv2._get_obs (ur3e_env2.py:111-123), lane 0 */
+KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
+  int st = m->id_site_tcp, sh = m->id_site_handle, gb = m->id_body_ghost;
+  const double* tcp = s.site_xpos[st];
+  const double* mug = s.site_xpos[sh];
+  const double* gh = s.xpos[gb];
+  double vt[6], vh[6];
+  w_site_velocity(m, s, st, vt);
+  w_site_velocity(m, s, sh, vh);
+  for (int k = 0; k < 3; k++) {
+    obs[k] = tcp[k];
+    obs[3 + k] = mug[k];
+    obs[6 + k] = gh[k];
+    obs[9 + k] = tcp[k] - mug[k];
+    obs[12 + k] = mug[k] - gh[k];
+    obs[15 + k] = vt[3 + k];
+    obs[18 + k] = vt[3 + k] - vh[3 + k];
+  }
+  obs[21] = s.qpos[6];
+  obs[22] = s.qvel[6];
+  int lp = 0, rp = 0;
+  for (int ci = 0; ci < s.ncon; ci++) {
+    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    if (!(b1 == m->id_body_fish || b2 == m->id_body_fish)) continue;
+    if (b1 == m->id_body_lpad || b2 == m->id_body_lpad) lp = 1;
+    if (b1 == m->id_body_rpad || b2 == m->id_body_rpad) rp = 1;
+  }
+  int robust = 0;
+  if (lp + rp == 2) {
+    double dx = fabs(tcp[0] - mug[0]), dy = fabs(tcp[1] - mug[1]), dz = fabs(tcp[2] - mug[2]);
+    robust = (dx < 0.01 && dy < 0.005 && dz < 0.05);
+  }
+  obs[23] = (double)robust;
+}
+
+KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
+  double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
+  if (1.0 < sqrt(dx * dx + dy * dy + dz * dz)) return 1;
+  for (int ci = 0; ci < s.ncon; ci++) {
+    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    int a1 = (m->mask_arm_bodies >> b1) & 1, a2 = (m->mask_arm_bodies >> b2) & 1;
+    if (a1 && a2) {
+      int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+      if (g1 && g2) continue;
+      return 1;
+    }
+  }
+  if (obs[5] <= m->fish_topple_z) return 1;
+  return 0;
+}
+
+struct WOut {
+  double obs[24];
+  double carry[NCARRY];
+  double a[8];
+  double r;
+  int term, trunc, t;
+};
+
+template <int NT>
+__device__ static void w_load(KModel m, const KState& st, int e, KS& s) {
+  const int tid = threadIdx.x;
+  for (int k = tid; k < m->nq; k += NT) s.qpos[k] = st.qpos[SQ(st, k, e)];
+  for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = st.qvel[SV(st, k, e)]; s.warm[k] = st.warm[SV(st, k, e)]; }
+  if (tid == 0) s.nwarn = st.nwarn[e];
+}
+
+template <int NT>
+__device__ static void w_store(KModel m, const KState& st, int e, const KS& s, const double* carry) {
+  const int tid = threadIdx.x;
+  for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
+  for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
+  for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = carry[k];
+  if (tid == 0) { st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn; }
+}
+
+/* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
+template <int NT>
+__device__ static void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
+                                   KS& s, WOut& o) {
+  const int tid = threadIdx.x;
+  for (int k = tid; k < m->nq; k += NT) s.qpos[k] = c.reset_key >= 0 ? m->key_qpos[c.reset_key][k] : m->qpos0[k];
+  for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = c.reset_key >= 0 ? m->key_qvel[c.reset_key][k] : 0.0; s.warm[k] = 0; }
+  for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
+  SYNC();
+  if (tid == 0) {
+    unsigned int ep = st.episode[e];
+    if (c.reset_noise && m->id_body_fish >= 0) {
+      unsigned int gid = (unsigned int)(c.env_id_offset + e);
+      double u0 = k_uniform01(c.seed, gid, ep, 0);
+      double u1 = k_uniform01(c.seed, gid, ep, 1);
+      s.qpos[14] += 0.0 + (0.02 - 0.0) * u0;
+      s.qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+    }
+    s.nwarn = 0;
+    st.t[e] = 0;
+    st.ep_len[e] = 0;
+    st.ep_return[e] = 0;
+    st.episode[e] = ep + 1;
+  }
+  SYNC();
+  w_forward<NT>(m, pl, s);
+  if (tid == 0 && c.task == UR3E_TASK_GYM_V2) w_obs_v2(m, s, o.obs);
+  w_make_carry<NT>(m, pl, s, o.carry);
+  SYNC();
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+                                                   KConfig c, KState st, const unsigned char* __restrict__ mask,
+                                                   double* __restrict__ obs_out) {
+  __shared__ KS s;
+  __shared__ WOut o;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  if (e >= st.n) return;
+  if (mask && !mask[e]) return;
+  w_reset_env<NT>(m, pl, c, st, e, s, o);
+  w_store<NT>(m, st, e, s, o.carry);
+  if (obs_out && c.task == UR3E_TASK_GYM_V2)
+    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+                                                  KConfig c, KState st, const double* __restrict__ actions, int adim,
+                                                  double* __restrict__ obs_out, double* __restrict__ rew_out,
+                                                  unsigned char* __restrict__ term_out,
+                                                  unsigned char* __restrict__ trunc_out,
+                                                  double* __restrict__ tobs_out) {
+  __shared__ KS s;
+  __shared__ WOut o;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  if (e >= st.n) return;
+  w_load<NT>(m, st, e, s);
+  for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
+  for (int k = tid; k < NCARRY; k += NT) o.carry[k] = st.carry[SC(st, k, e)];
+  SYNC();
+  if (tid == 0) {
+    double ctrl[K_NU];
+    if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
+      double traj[7];
+      if (c.task == UR3E_TASK_GYM_V2) {
+        traj[0] = o.a[0]; traj[1] = o.a[1]; traj[2] = o.a[2];
+        traj[3] = -1.209; traj[4] = -1.209; traj[5] = 1.209;
+        traj[6] = o.a[3];
+      } else {
+        for (int k = 0; k < 7; k++) traj[k] = o.a[k];
+      }
+      double out[7];
+      k_pid_task_ctrl(traj, o.carry, s.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
+      for (int k = 0; k < 6; k++) ctrl[k] = out[k];
+      if (m->nu > 6) ctrl[6] = out[6];
+    } else if (c.task == UR3E_TASK_MOVE_J) {
+      for (int k = 0; k < 6; k++) {
+        double q = s.qpos[k];
+        double delta = o.a[k] - q;
+        double t = q + delta;
+        if (t < m->jnt_range[k][0]) t = m->jnt_range[k][0];
+        if (t > m->jnt_range[k][1]) t = m->jnt_range[k][1];
+        double er = t - q;
+        double uk = c.gains.joint[k] * er + c.gains.joint[6 + k] * (-s.qvel[k]);
+        if (uk < m->act_ctrlrange[k][0]) uk = m->act_ctrlrange[k][0];
+        if (uk > m->act_ctrlrange[k][1]) uk = m->act_ctrlrange[k][1];
+        ctrl[k] = uk;
+      }
+      if (m->nu > 6) ctrl[6] = o.a[6] * m->act_ctrlrange[m->nu - 1][1];
+    } else {
+      for (int k = 0; k < m->nu; k++) ctrl[k] = o.a[k];
+    }
+    for (int k = 0; k < m->nu; k++) s.ctrl[k] = ctrl[k];
+  }
+  SYNC();
+  int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  for (int sstep = 0; sstep < fs; sstep++) w_step<NT>(m, pl, s);
+  w_make_carry<NT>(m, pl, s, o.carry);
+  SYNC();
+  if (c.task != UR3E_TASK_GYM_V2) {
+    if (tid == 0) { st.t[e] += 1; st.ep_len[e] += 1; }
+    w_store<NT>(m, st, e, s, o.carry);
+    return;
+  }
+  if (tid == 0) {
+    int t = st.t[e] + 1;
+    st.t[e] = t;
+    w_obs_v2(m, s, o.obs);
+    double r = k_reward_v2(o.obs, o.a);
+    int term = w_termination_v2(m, s, o.obs);
+    int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
+    double dx = o.obs[3] - o.obs[6], dy = o.obs[4] - o.obs[7], dz = o.obs[5] - o.obs[8];
+    if (sqrt(dx * dx + dy * dy + dz * dz) < 0.05) {
+      term = 1;
+      r += 50.0;
+    }
+    st.ep_return[e] += r;
+    st.ep_len[e] += 1;
+    if (rew_out) rew_out[e] = r;
+    if (term_out) term_out[e] = (unsigned char)term;
+    if (trunc_out) trunc_out[e] = (unsigned char)trunc;
+    o.term = term;
+    o.trunc = trunc;
+  }
+  SYNC();
+  if ((o.term || o.trunc) && c.auto_reset) {
+    if (tobs_out)
+      for (int k = tid; k < 24; k += NT) tobs_out[(size_t)e * 24 + k] = o.obs[k];
+    SYNC();
+    w_reset_env<NT>(m, pl, c, st, e, s, o);
+  }
+  w_store<NT>(m, st, e, s, o.carry);
+  if (obs_out)
+    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void w_env_set_state(const ur3e_model_t* __restrict__ m,
+                                                       const KPlan* __restrict__ pl, KConfig c, KState st,
+                                                       const double* __restrict__ qpos,
+                                                       const double* __restrict__ qvel,
+                                                       const double* __restrict__ warm) {
+  __shared__ KS s;
+  __shared__ WOut o;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  if (e >= st.n) return;
+  for (int k = tid; k < m->nq; k += NT) s.qpos[k] = qpos[(size_t)e * m->nq + k];
+  for (int k = tid; k < m->nv; k += NT) {
+    s.qvel[k] = qvel[(size_t)e * m->nv + k];
+    s.warm[k] = warm ? warm[(size_t)e * m->nv + k] : st.warm[SV(st, k, e)];
+  }
+  for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
+  if (tid == 0) s.nwarn = st.nwarn[e];
+  SYNC();
+  w_forward<NT>(m, pl, s);
+  w_make_carry<NT>(m, pl, s, o.carry);
+  SYNC();
+  w_store<NT>(m, st, e, s, o.carry);
+}
+
 /* create(): qpos0 / zero velocities, episode 0; envs are valid after ur3e_batch_reset */
 __global__ void k_env_init(const ur3e_model_t* __restrict__ m, KState s) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= s.n) return;
-  const int n = s.n;
-  for (int k = 0; k < m->nq; k++) s.qpos[(size_t)k * n + e] = m->qpos0[k];
-  for (int k = 0; k < m->nv; k++) { s.qvel[(size_t)k * n + e] = 0; s.warm[(size_t)k * n + e] = 0; }
-  for (int k = 0; k < NCARRY; k++) s.carry[(size_t)k * n + e] = 0;
+  for (int k = 0; k < m->nq; k++) s.qpos[SQ(s, k, e)] = m->qpos0[k];
+  for (int k = 0; k < m->nv; k++) { s.qvel[SV(s, k, e)] = 0; s.warm[SV(s, k, e)] = 0; }
+  for (int k = 0; k < NCARRY; k++) s.carry[SC(s, k, e)] = 0;
   s.t[e] = 0; s.episode[e] = 0; s.ep_len[e] = 0; s.ep_return[e] = 0; s.ncon[e] = 0; s.nwarn[e] = 0;
 }
 
@@ -471,13 +764,12 @@ __global__ void k_env_get_state(int nq, int nv, KState s, double* __restrict__ q
                                 double* __restrict__ warm) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= s.n) return;
-  const int n = s.n;
   if (qpos)
-    for (int k = 0; k < nq; k++) qpos[(size_t)e * nq + k] = s.qpos[(size_t)k * n + e];
+    for (int k = 0; k < nq; k++) qpos[(size_t)e * nq + k] = s.qpos[SQ(s, k, e)];
   if (qvel)
-    for (int k = 0; k < nv; k++) qvel[(size_t)e * nv + k] = s.qvel[(size_t)k * n + e];
+    for (int k = 0; k < nv; k++) qvel[(size_t)e * nv + k] = s.qvel[SV(s, k, e)];
   if (warm)
-    for (int k = 0; k < nv; k++) warm[(size_t)e * nv + k] = s.warm[(size_t)k * n + e];
+    for (int k = 0; k < nv; k++) warm[(size_t)e * nv + k] = s.warm[SV(s, k, e)];
 }
 
 __global__ void k_env_get_info(KState s, int* ncon, int* ep_len, double* ep_ret, int* nwarn) {
@@ -495,8 +787,10 @@ __global__ void k_env_get_info(KState s, int* ncon, int* ep_len, double* ep_ret,
 struct ur3e_batch {
   int device;
   int n;
+  int wave_nt; /* 0: lane-per-env kernels (v1); 64/128: workgroup-per-env kernels (v2) */
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
+  KPlan* d_plan;
   KConfig cfg;
   KState st;
   hipEvent_t ev0, ev1;
@@ -528,6 +822,36 @@ static int check_model(const ur3e_model_t* m) {
   return UR3E_OK;
 }
 
+static void build_plan(const ur3e_model_t* m, KPlan* pl) {
+  memset(pl, 0, sizeof(*pl));
+  int nl = 0;
+  for (int i = 1; i < m->nbody; i++) {
+    pl->body_depth[i] = pl->body_depth[m->body_parentid[i]] + 1;
+    if (pl->body_depth[i] > nl) nl = pl->body_depth[i];
+  }
+  pl->nlevel = nl;
+  for (int i = 0; i < m->nv; i++) {
+    int na = 0;
+    unsigned int mask = 0;
+    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) {
+      pl->dof_anc[i][na++] = j;
+      mask |= 1u << j;
+    }
+    pl->dof_nanc[i] = na;
+    pl->dof_anc_mask[i] = mask;
+  }
+  for (int b = 0; b < m->nbody; b++) {
+    int dof = -1;
+    for (int q = b; q > 0 && dof < 0; q = m->body_parentid[q])
+      if (m->body_dofnum[q]) dof = m->body_dofadr[q] + m->body_dofnum[q] - 1;
+    unsigned int mask = 0;
+    for (int j = dof; j >= 0; j = m->dof_parentid[j]) mask |= 1u << j;
+    pl->body_dof_mask[b] = mask;
+  }
+  for (int v = 0; v < m->nv; v++)
+    if (m->dof_frictionloss[v] > 0) pl->floss_dof[pl->nfloss++] = v;
+}
+
 extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
                                  ur3e_batch_t** out) {
   if (!model || !cfg || !out || n_envs <= 0) return fail(UR3E_EINVAL, "null argument or n_envs <= 0");
@@ -540,10 +864,13 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   if ((cfg->task == UR3E_TASK_GYM_V2 || cfg->task == UR3E_TASK_TRAJ_L) && model->id_site_tcp < 0)
     return fail(UR3E_EMODEL, "task-space control needs the tcp site");
   if (cfg->reset_key >= model->nkey) return fail(UR3E_EINVAL, "reset_key out of range");
+  int wave_nt = cfg->envs_per_block == 0 ? 128 : (cfg->envs_per_block == -64 ? 64 : (cfg->envs_per_block < 0 ? 128 : 0));
+  if (wave_nt && model->ncpair > W_MAXCAND) return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
   HIPCHK(hipSetDevice(device));
   ur3e_batch* b = new ur3e_batch();
   b->device = device;
   b->n = n_envs;
+  b->wave_nt = wave_nt;
   b->host_model = *model;
   b->timed = 0;
   KConfig& c = b->cfg;
@@ -556,12 +883,21 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.seed = cfg->seed;
   c.env_id_offset = cfg->env_id_offset;
   c.epb = cfg->envs_per_block > 0 && cfg->envs_per_block <= 64 ? cfg->envs_per_block : 16;
+  KPlan plan;
+  build_plan(model, &plan);
   for (int k = 0; k < 12; k++) { c.gains.task[k] = cfg->task_gains[k]; c.gains.joint[k] = cfg->joint_gains[k]; }
   KState& s = b->st;
   s.n = n_envs;
+  if (wave_nt) {
+    s.fs = 1; s.es_q = model->nq; s.es_v = model->nv; s.es_c = NCARRY;
+  } else {
+    s.fs = n_envs; s.es_q = 1; s.es_v = 1; s.es_c = 1;
+  }
   size_t nd = (size_t)n_envs;
   HIPCHK(hipMalloc(&b->d_model, sizeof(ur3e_model_t)));
   HIPCHK(hipMemcpy(b->d_model, model, sizeof(ur3e_model_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&b->d_plan, sizeof(KPlan)));
+  HIPCHK(hipMemcpy(b->d_plan, &plan, sizeof(KPlan), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&s.qpos, sizeof(double) * nd * model->nq));
   HIPCHK(hipMalloc(&s.qvel, sizeof(double) * nd * model->nv));
   HIPCHK(hipMalloc(&s.warm, sizeof(double) * nd * model->nv));
@@ -587,7 +923,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
 extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
-  void* bufs[] = {b->d_model, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
+  void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
                   b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn};
   for (void* p : bufs) (void)hipFree(p);
   (void)hipEventDestroy(b->ev0);
@@ -601,8 +937,15 @@ static int grid_of(const ur3e_batch* b) { return (b->n + b->cfg.epb - 1) / b->cf
 extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* d_obs, void* stream) {
   if (!b) return fail(UR3E_EINVAL, "null handle");
   HIPCHK(hipSetDevice(b->device));
-  hipLaunchKernelGGL(k_env_reset, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg, b->st,
-                     d_mask, d_obs);
+  if (b->wave_nt == 128)
+    hipLaunchKernelGGL(w_env_reset<128>, dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model, b->d_plan, b->cfg,
+                       b->st, d_mask, d_obs);
+  else if (b->wave_nt == 64)
+    hipLaunchKernelGGL(w_env_reset<64>, dim3(b->n), dim3(64), 0, (hipStream_t)stream, b->d_model, b->d_plan, b->cfg,
+                       b->st, d_mask, d_obs);
+  else
+    hipLaunchKernelGGL(k_env_reset, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg, b->st,
+                       d_mask, d_obs);
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }
@@ -615,8 +958,15 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   HIPCHK(hipSetDevice(b->device));
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipEventRecord(b->ev0, st));
-  hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
-                     d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+  if (b->wave_nt == 128)
+    hipLaunchKernelGGL(w_env_step<128>, dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st, d_actions,
+                       adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+  else if (b->wave_nt == 64)
+    hipLaunchKernelGGL(w_env_step<64>, dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st, d_actions,
+                       adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+  else
+    hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
+                       d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->ev1, st));
   b->timed = 1;
@@ -636,8 +986,15 @@ extern "C" int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const
                                     const double* d_warm, void* stream) {
   if (!b || !d_qpos || !d_qvel) return fail(UR3E_EINVAL, "null handle or state");
   HIPCHK(hipSetDevice(b->device));
-  hipLaunchKernelGGL(k_env_set_state, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg,
-                     b->st, d_qpos, d_qvel, d_warm);
+  if (b->wave_nt == 128)
+    hipLaunchKernelGGL(w_env_set_state<128>, dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model, b->d_plan,
+                       b->cfg, b->st, d_qpos, d_qvel, d_warm);
+  else if (b->wave_nt == 64)
+    hipLaunchKernelGGL(w_env_set_state<64>, dim3(b->n), dim3(64), 0, (hipStream_t)stream, b->d_model, b->d_plan,
+                       b->cfg, b->st, d_qpos, d_qvel, d_warm);
+  else
+    hipLaunchKernelGGL(k_env_set_state, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg,
+                       b->st, d_qpos, d_qvel, d_warm);
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }

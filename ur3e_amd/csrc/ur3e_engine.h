@@ -476,8 +476,13 @@ KD void k_solve_tree(KModel m, const double A[K_NV][K_NV], const double diaginv[
   for (int i = nv - 1; i >= 0; i--)
     for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) x[j] -= A[i][j] * x[i];
   for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
-  for (int i = 0; i < nv; i++)
-    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) x[i] -= A[i][j] * x[j];
+  /* forward pass: ancestors farthest-first (increasing index), so the GPU can run it as a
+     column sweep with the same per-element operation order */
+  for (int i = 0; i < nv; i++) {
+    int anc[UR3E_MAXNV], na = 0;
+    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) anc[na++] = j;
+    for (int t = na - 1; t >= 0; t--) x[i] -= A[i][anc[t]] * x[anc[t]];
+  }
 }
 
 /* r = M v, dense row order (exact zeros add nothing) */
@@ -854,6 +859,7 @@ KDN void k_make_constraint(KModel m, KData* d) {
       k_jac_point(m, d, b1, p1, jp1, nullptr);
       k_jac_point(m, d, b2, p2, jp2, nullptr);
       double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      if (d->nefc + 3 > K_MAXEFC) return;
       for (int k = 0; k < 3; k++) {
         int r = k_add_row(d, CN_EQUALITY, e, 0);
         if (r < 0) return;
@@ -919,6 +925,7 @@ KDN void k_make_constraint(KModel m, KData* d) {
     k_jac_point(m, d, b2, c->pos, jp2, nullptr);
     double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
     double incl = m->cpair_margin[p] - m->cpair_gap[p];
+    if (d->nefc + 3 > K_MAXEFC) return;
     c->efc_address = d->nefc;
     for (int k = 0; k < 3; k++) {
       int r = k_add_row(d, CN_CONTACT_ELLIPTIC, ci, 0);
@@ -1249,7 +1256,7 @@ KD void k_hessian_solve(KModel m, const KData* d, double* x, const double* b) {
   }
   for (int i = nv - 1; i >= 0; i--) {
     double v = x[i];
-    for (int k = i + 1; k < nv; k++) v -= d->H[k][i] * x[k];
+    for (int k = nv - 1; k > i; k--) v -= d->H[k][i] * x[k];
     x[i] = v / d->H[i][i];
   }
 }

@@ -1,0 +1,1277 @@
+/*
+ * ur3e_wave.h — v2 step engine: ONE WORKGROUP (NT = 64 or 128 lanes) PER ENV,
+ * the env's whole working set staged in LDS (KS, ~77 KB: two envs per CU).
+ *
+ * Why: the v1 layout (one env per lane, ~80 KB lane-private scratch) spills to
+ * HBM — rocprofv3 measured ~330 KB of fetches per env-step and every dependent
+ * access waiting on a miss (profiles/r01_v1_lane_per_env).  Here the same
+ * arithmetic runs as cooperative lane-parallel stages over LDS:
+ *   - tree passes (kinematics, com velocity, RNE forward) run level by level,
+ *     one lane per body; subtree accumulations run one lane per component;
+ *   - mass matrix rows, constraint row groups, collision candidates, Hessian
+ *     elements, Newton vectors: one lane per output element;
+ *   - the tree LDL' and both triangular solves run as column sweeps;
+ *   - every serial reduction the oracle performs in a given order (costs,
+ *     line-search sums, norms) is done by lane 0 over per-row contributions
+ *     staged in LDS, in the oracle's order.
+ * Parallelising over OUTPUT elements only, never splitting a sum, keeps every
+ * result bit-identical to the CPU oracle (oracle/ur3e_oracle.c).
+ *
+ * Semantics: MuJoCo 3.3.3 mj_step (see ur3e_engine.h for the stage list) as
+ * driven by gymnasium_env/envs/ur3e_env2.py:72-99.
+ */
+#ifndef UR3E_WAVE_H
+#define UR3E_WAVE_H
+
+#include "ur3e_engine.h"
+
+#define W_MAXCAND 128 /* collision candidates handled per env (main.xml: 92) */
+#define W_MAXGRP 96   /* constraint row groups */
+
+/* host-precomputed tree bookkeeping for the cooperative stages */
+struct KPlan {
+  int nlevel;
+  int body_depth[K_NB];
+  unsigned int dof_anc_mask[K_NV]; /* bit j: j is a proper ancestor of dof i */
+  int dof_nanc[K_NV];
+  int dof_anc[K_NV][K_NV];         /* proper ancestors, nearest first */
+  unsigned int body_dof_mask[K_NB];
+  int nfloss;
+  int floss_dof[K_NV];
+  int neq_rows;
+};
+
+/* constraint row groups (one lane builds one group) */
+#define G_CONNECT 0
+#define G_JOINTEQ 1
+#define G_FLOSS 2
+#define G_LIMIT 3
+#define G_CONTACT 4
+
+struct KS {
+  /* state */
+  double qpos[K_NQ], qvel[K_NV], warm[K_NV], ctrl[K_NU];
+  /* position stage */
+  double xpos[K_NB][3], xquat[K_NB][4], xmat[K_NB][9];
+  double xanchor[K_NJ][3], xaxis[K_NJ][3];
+  double geom_xpos[K_NG][3], geom_xmat[K_NG][9];
+  double site_xpos[K_NS][3], site_xmat[K_NS][9];
+  double subtree_com[K_NB][3], cinert[K_NB][10], cdof[K_NV][6];
+  double cvel[K_NB][6], cdof_dot[K_NV][6];
+  double actuator_length[K_NU], act_force[K_NU];
+  double qM[K_NV][K_NV], qLD[K_NV][K_NV], LDinv[K_NV], H[K_NV][K_NV];
+  /* vectors */
+  double qfrc_bias[K_NV], qfrc_passive[K_NV], qfrc_smooth[K_NV], qacc_smooth[K_NV], qacc[K_NV];
+  double qfrc_constraint[K_NV], Ma[K_NV], grad[K_NV], search[K_NV], Mv[K_NV], xv[K_NV], fv[K_NV];
+  double tmpv[K_NV];
+  /* body temporaries (crb / cacc / cfrc) aliased with per-row Newton temporaries */
+  union {
+    struct {
+      double b10[K_NB][10];
+      double b6[K_NB][6];
+    } body;
+    struct {
+      double F[K_MAXEFC], dF[K_MAXEFC], d2F[K_MAXEFC];
+    } row;
+  } u;
+  /* contacts */
+  double con_pos[K_MAXCON][3], con_frame[K_MAXCON][9], con_dist[K_MAXCON], con_mu[K_MAXCON];
+  double con_Hc[K_MAXCON][9];
+  int con_geom1[K_MAXCON], con_geom2[K_MAXCON], con_cpair[K_MAXCON], con_efc[K_MAXCON];
+  int cand_count[W_MAXCAND], cand_off[W_MAXCAND];
+  /* constraint rows */
+  double efc_J[K_MAXEFC][K_NV];
+  double efc_R[K_MAXEFC], efc_D[K_MAXEFC], efc_aref[K_MAXEFC], efc_floss[K_MAXEFC];
+  double efc_force[K_MAXEFC], jar[K_MAXEFC], Jv[K_MAXEFC];
+  int efc_type[K_MAXEFC], efc_id[K_MAXEFC], efc_state[K_MAXEFC], rowflag[K_MAXEFC];
+  int grp_type[W_MAXGRP], grp_id[W_MAXGRP], grp_row[W_MAXGRP];
+  /* scalars */
+  double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
+  int ncon, nefc, ngrp, nwarn, flag;
+};
+
+#define SYNC() __syncthreads()
+
+/* ================================================================== */
+/* kinematics (level-parallel over bodies)                             */
+/* ================================================================== */
+template <int NT>
+__device__ static void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
+    s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
+    k_quat2mat(s.xmat[0], s.xquat[0]);
+  }
+  SYNC();
+  const int nb = m->nbody;
+  for (int lvl = 1; lvl <= pl->nlevel; lvl++) {
+    for (int i = tid; i < nb; i += NT) {
+      if (i == 0 || pl->body_depth[i] != lvl) continue;
+      int pid = m->body_parentid[i];
+      double xpos[3], xquat[4];
+      int jfirst = m->body_jntadr[i];
+      if (m->body_jntnum[i] == 1 && m->jnt_type[jfirst] == UR3E_JNT_FREE) {
+        int a = m->jnt_qposadr[jfirst];
+        xpos[0] = s.qpos[a]; xpos[1] = s.qpos[a + 1]; xpos[2] = s.qpos[a + 2];
+        xquat[0] = s.qpos[a + 3]; xquat[1] = s.qpos[a + 4]; xquat[2] = s.qpos[a + 5]; xquat[3] = s.qpos[a + 6];
+        k_normalize4(xquat);
+        s.xanchor[jfirst][0] = xpos[0]; s.xanchor[jfirst][1] = xpos[1]; s.xanchor[jfirst][2] = xpos[2];
+        s.xaxis[jfirst][0] = 0; s.xaxis[jfirst][1] = 0; s.xaxis[jfirst][2] = 1;
+      } else {
+        double t[3];
+        k_mat_vec3(t, s.xmat[pid], m->body_pos[i]);
+        xpos[0] = s.xpos[pid][0] + t[0]; xpos[1] = s.xpos[pid][1] + t[1]; xpos[2] = s.xpos[pid][2] + t[2];
+        k_mul_quat(xquat, s.xquat[pid], m->body_quat[i]);
+        for (int k = 0; k < m->body_jntnum[i]; k++) {
+          int j = jfirst + k;
+          double xaxis[3], xanchor[3], qloc[4], vec[3];
+          k_rot_vec_quat(xaxis, m->jnt_axis[j], xquat);
+          k_rot_vec_quat(xanchor, m->jnt_pos[j], xquat);
+          xanchor[0] += xpos[0]; xanchor[1] += xpos[1]; xanchor[2] += xpos[2];
+          int a = m->jnt_qposadr[j];
+          k_axis_angle_quat(qloc, m->jnt_axis[j], s.qpos[a] - m->qpos0[a]);
+          k_mul_quat(xquat, xquat, qloc);
+          k_rot_vec_quat(vec, m->jnt_pos[j], xquat);
+          xpos[0] = xanchor[0] - vec[0]; xpos[1] = xanchor[1] - vec[1]; xpos[2] = xanchor[2] - vec[2];
+          for (int c = 0; c < 3; c++) { s.xanchor[j][c] = xanchor[c]; s.xaxis[j][c] = xaxis[c]; }
+        }
+      }
+      k_normalize4(xquat);
+      for (int c = 0; c < 3; c++) s.xpos[i][c] = xpos[c];
+      for (int c = 0; c < 4; c++) s.xquat[i][c] = xquat[c];
+      k_quat2mat(s.xmat[i], xquat);
+    }
+    SYNC();
+  }
+  for (int g = tid; g < m->ngeom + m->nsite; g += NT) {
+    if (g < m->ngeom) {
+      int b = m->geom_bodyid[g];
+      k_local2global(s.geom_xpos[g], s.geom_xmat[g], s.xpos[b], s.xquat[b], s.xmat[b], m->geom_pos[g],
+                     m->geom_quat[g]);
+    } else {
+      int q = g - m->ngeom;
+      int b = m->site_bodyid[q];
+      k_local2global(s.site_xpos[q], s.site_xmat[q], s.xpos[b], s.xquat[b], s.xmat[b], m->site_pos[q],
+                     m->site_quat[q]);
+    }
+  }
+  SYNC();
+}
+
+/* ================================================================== */
+/* com_pos: subtree com, cinert, cdof                                  */
+/* ================================================================== */
+template <int NT>
+__device__ static void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nb = m->nbody;
+  double xipos[3] = {0, 0, 0}, ximat[9];
+  if (tid < nb) {
+    int i = tid;
+    if (i == 0) {
+      k_quat2mat(ximat, s.xquat[0]);
+    } else {
+      k_local2global(xipos, ximat, s.xpos[i], s.xquat[i], s.xmat[i], m->body_ipos[i], m->body_iquat[i]);
+    }
+    s.subtree_com[i][0] = xipos[0] * m->body_mass[i];
+    s.subtree_com[i][1] = xipos[1] * m->body_mass[i];
+    s.subtree_com[i][2] = xipos[2] * m->body_mass[i];
+  }
+  SYNC();
+  if (tid < 3) {
+    for (int i = nb - 1; i > 0; i--) s.subtree_com[m->body_parentid[i]][tid] += s.subtree_com[i][tid];
+  }
+  SYNC();
+  if (tid < nb) {
+    int i = tid;
+    if (m->body_subtreemass[i] < K_MINVAL) {
+      s.subtree_com[i][0] = xipos[0]; s.subtree_com[i][1] = xipos[1]; s.subtree_com[i][2] = xipos[2];
+    } else {
+      double sc = 1.0 / m->body_subtreemass[i];
+      s.subtree_com[i][0] *= sc; s.subtree_com[i][1] *= sc; s.subtree_com[i][2] *= sc;
+    }
+  }
+  SYNC();
+  if (tid < nb) {
+    int i = tid;
+    double* r = s.cinert[i];
+    if (i == 0) {
+      for (int k = 0; k < 10; k++) r[k] = 0;
+    } else {
+      const double* mat = ximat;
+      const double* in = m->body_inertia[i];
+      const double* c = s.subtree_com[m->body_rootid[i]];
+      double dif[3] = {xipos[0] - c[0], xipos[1] - c[1], xipos[2] - c[2]};
+      double mass = m->body_mass[i];
+      double tmp[9] = {mat[0] * in[0], mat[3] * in[0], mat[6] * in[0], mat[1] * in[1], mat[4] * in[1],
+                       mat[7] * in[1], mat[2] * in[2], mat[5] * in[2], mat[8] * in[2]};
+      r[0] = mat[0] * tmp[0] + mat[1] * tmp[3] + mat[2] * tmp[6];
+      r[1] = mat[3] * tmp[1] + mat[4] * tmp[4] + mat[5] * tmp[7];
+      r[2] = mat[6] * tmp[2] + mat[7] * tmp[5] + mat[8] * tmp[8];
+      r[3] = mat[0] * tmp[1] + mat[1] * tmp[4] + mat[2] * tmp[7];
+      r[4] = mat[0] * tmp[2] + mat[1] * tmp[5] + mat[2] * tmp[8];
+      r[5] = mat[3] * tmp[2] + mat[4] * tmp[5] + mat[5] * tmp[8];
+      r[0] += mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+      r[1] += mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+      r[2] += mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+      r[3] -= mass * dif[0] * dif[1];
+      r[4] -= mass * dif[0] * dif[2];
+      r[5] -= mass * dif[1] * dif[2];
+      r[6] = mass * dif[0];
+      r[7] = mass * dif[1];
+      r[8] = mass * dif[2];
+      r[9] = mass;
+    }
+  }
+  for (int j = tid; j < m->njnt; j += NT) {
+    int b = m->jnt_bodyid[j];
+    int da = m->jnt_dofadr[j];
+    const double* c = s.subtree_com[m->body_rootid[b]];
+    double off[3] = {c[0] - s.xanchor[j][0], c[1] - s.xanchor[j][1], c[2] - s.xanchor[j][2]};
+    if (m->jnt_type[j] == UR3E_JNT_FREE) {
+      for (int k = 0; k < 3; k++) {
+        for (int r = 0; r < 6; r++) s.cdof[da + k][r] = 0;
+        s.cdof[da + k][3 + k] = 1;
+      }
+      for (int k = 0; k < 3; k++) {
+        double ax[3] = {s.xmat[b][k], s.xmat[b][3 + k], s.xmat[b][6 + k]};
+        double cr[3];
+        k_cross3(cr, ax, off);
+        s.cdof[da + 3 + k][0] = ax[0]; s.cdof[da + 3 + k][1] = ax[1]; s.cdof[da + 3 + k][2] = ax[2];
+        s.cdof[da + 3 + k][3] = cr[0]; s.cdof[da + 3 + k][4] = cr[1]; s.cdof[da + 3 + k][5] = cr[2];
+      }
+    } else {
+      double cr[3];
+      k_cross3(cr, s.xaxis[j], off);
+      s.cdof[da][0] = s.xaxis[j][0]; s.cdof[da][1] = s.xaxis[j][1]; s.cdof[da][2] = s.xaxis[j][2];
+      s.cdof[da][3] = cr[0]; s.cdof[da][4] = cr[1]; s.cdof[da][5] = cr[2];
+    }
+  }
+  for (int a = tid; a < m->nu; a += NT) {
+    double g = m->act_gear[a];
+    if (m->act_trntype[a] == UR3E_TRN_JOINT) {
+      s.actuator_length[a] = s.qpos[m->jnt_qposadr[m->act_trnid[a]]] * g;
+    } else {
+      int t = m->act_trnid[a];
+      double len = 0;
+      for (int k = 0; k < m->ten_num[t]; k++) len += m->ten_coef[t][k] * s.qpos[k_dof_qposadr(m, m->ten_dof[t][k])];
+      s.actuator_length[a] = len * g;
+    }
+  }
+  SYNC();
+}
+
+/* ================================================================== */
+/* CRB mass matrix + tree LDL'                                         */
+/* ================================================================== */
+template <int NT>
+__device__ static void w_crb(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nb = m->nbody, nv = m->nv;
+  for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
+  for (int e = tid; e < nv * nv; e += NT) s.qM[e / nv][e % nv] = 0;
+  SYNC();
+  if (tid < 10) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m->body_parentid[i];
+      if (p > 0) s.u.body.b10[p][tid] += s.u.body.b10[i][tid];
+    }
+  }
+  SYNC();
+  if (tid < nv) {
+    int i = tid;
+    double buf[6];
+    k_mul_inert_vec(buf, s.u.body.b10[m->dof_bodyid[i]], s.cdof[i]);
+    double mii = m->dof_armature[i];
+    mii += k_dot6(s.cdof[i], buf);
+    s.qM[i][i] = mii;
+    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) {
+      double v = 0.0;
+      v += k_dot6(s.cdof[j], buf);
+      s.qM[i][j] = v;
+      s.qM[j][i] = v;
+    }
+  }
+  SYNC();
+}
+
+/* A (K_NV x K_NV in LDS) -> reverse tree LDL' in place, diaginv */
+template <int NT>
+__device__ static void w_factor_tree(KModel m, const KPlan* __restrict__ pl, double (*A)[K_NV], double* diaginv,
+                                     double* tmp) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  for (int k = nv - 1; k >= 0; k--) {
+    const int na = pl->dof_nanc[k];
+    if (na == 0) {
+      if (tid == 0 && A[k][k] < K_MINVAL) A[k][k] = K_MINVAL;
+      continue;
+    }
+    if (tid == 0 && A[k][k] < K_MINVAL) A[k][k] = K_MINVAL;
+    SYNC();
+    if (tid < na) tmp[tid] = A[k][pl->dof_anc[k][tid]] / A[k][k];
+    SYNC();
+    const int npair = na * (na + 1) / 2;
+    for (int e = tid; e < npair; e += NT) {
+      int p = 0, rem = e;
+      while (rem >= na - p) { rem -= na - p; p++; }
+      int q = p + rem;
+      int i = pl->dof_anc[k][p], j = pl->dof_anc[k][q];
+      A[i][j] -= A[k][j] * tmp[p];
+    }
+    SYNC();
+    if (tid < na) A[k][pl->dof_anc[k][tid]] = tmp[tid];
+    SYNC();
+  }
+  SYNC();
+  for (int i = tid; i < nv; i += NT) diaginv[i] = 1.0 / A[i][i];
+  SYNC();
+}
+
+/* x = A^-1 b with the tree factor; x, b in LDS (may alias) */
+template <int NT>
+__device__ static void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K_NV],
+                                    const double* diaginv, double* x, const double* b) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  if (tid < nv) x[tid] = b[tid];
+  SYNC();
+  for (int i = nv - 1; i >= 0; i--) {
+    if (pl->dof_nanc[i] == 0) continue;
+    if (tid < nv && ((pl->dof_anc_mask[i] >> tid) & 1u)) x[tid] -= A[i][tid] * x[i];
+    SYNC();
+  }
+  if (tid < nv) x[tid] *= diaginv[tid];
+  SYNC();
+  for (int j = 0; j < nv; j++) {
+    if (tid < nv && ((pl->dof_anc_mask[tid] >> j) & 1u)) x[tid] -= A[tid][j] * x[j];
+    SYNC();
+  }
+}
+
+/* ================================================================== */
+/* collision: per-candidate lanes, prefix offsets, deterministic order */
+/* ================================================================== */
+__device__ static int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
+  int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
+  double margin = m->cpair_margin[p];
+  double rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
+  if (rb1 > 0 && rb2 > 0) {
+    double dx = s.geom_xpos[g1][0] - s.geom_xpos[g2][0];
+    double dy = s.geom_xpos[g1][1] - s.geom_xpos[g2][1];
+    double dz = s.geom_xpos[g1][2] - s.geom_xpos[g2][2];
+    double lim = rb1 + rb2 + margin;
+    if (dx * dx + dy * dy + dz * dz > lim * lim) return 0;
+  }
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
+    return k_plane_box(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2], margin,
+                       raw);
+  if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX)
+    return k_box_box(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
+                     m->geom_size[g2], margin, raw);
+  return 0;
+}
+
+template <int NT>
+__device__ static void w_collision(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int np = m->ncpair;
+  KRaw raw[8];
+  for (int p = tid; p < np; p += NT) s.cand_count[p] = w_narrow(m, s, p, raw);
+  SYNC();
+  if (tid == 0) {
+    int off = 0;
+    for (int p = 0; p < np; p++) {
+      s.cand_off[p] = off;
+      off += s.cand_count[p];
+    }
+    s.ncon = off < K_MAXCON ? off : K_MAXCON;
+  }
+  SYNC();
+  for (int p = tid; p < np; p += NT) {
+    int cnt = s.cand_count[p];
+    int off = s.cand_off[p];
+    if (cnt == 0 || off >= K_MAXCON) continue;
+    int n = w_narrow(m, s, p, raw);
+    for (int k = 0; k < n && off + k < K_MAXCON; k++) {
+      int c = off + k;
+      s.con_pos[c][0] = raw[k].pos[0]; s.con_pos[c][1] = raw[k].pos[1]; s.con_pos[c][2] = raw[k].pos[2];
+      k_make_frame(s.con_frame[c], raw[k].n);
+      s.con_dist[c] = raw[k].dist;
+      s.con_geom1[c] = m->cpair_geom1[p];
+      s.con_geom2[c] = m->cpair_geom2[p];
+      s.con_cpair[c] = p;
+      s.con_mu[c] = 0;
+      s.con_efc[c] = -1;
+    }
+  }
+  SYNC();
+}
+
+/* ================================================================== */
+/* constraint rows                                                     */
+/* ================================================================== */
+/* translational point-Jacobian column v of `body` at p (zero outside the chain) */
+KD void w_jacp_col(KModel m, const KPlan* __restrict__ pl, const KS& s, int body, const double off[3], int v,
+                   double out[3]) {
+  if ((pl->body_dof_mask[body] >> v) & 1u) {
+    const double* cd = s.cdof[v];
+    double cr[3];
+    k_cross3(cr, cd, off);
+    out[0] = cd[3] + cr[0];
+    out[1] = cd[4] + cr[1];
+    out[2] = cd[5] + cr[2];
+  } else {
+    out[0] = 0; out[1] = 0; out[2] = 0;
+  }
+}
+
+KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double* simp, double pos, double margin,
+                        double diag, int friction_row) {
+  const int nv = m->nv;
+  double vel = 0;
+  for (int k = 0; k < nv; k++) vel += s.efc_J[r][k] * s.qvel[k];
+  double imp = k_get_impedance(simp, pos, margin);
+  double dmax = simp[1];
+  if (dmax < K_MINIMP) dmax = K_MINIMP;
+  if (dmax > K_MAXIMP) dmax = K_MAXIMP;
+  double K, B;
+  if (sref[0] > 0) {
+    double tc = sref[0];
+    if (tc < 2 * m->timestep) tc = 2 * m->timestep;
+    double dr = sref[1];
+    K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+    B = 2.0 / (dmax * tc);
+  } else {
+    K = -sref[0] / (dmax * dmax);
+    B = -sref[1] / dmax;
+  }
+  if (friction_row)
+    s.efc_aref[r] = -B * vel;
+  else
+    s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
+  double R = (1 - imp) * diag / imp;
+  s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
+}
+
+template <int NT>
+__device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  /* lane 0 lays out the row groups in oracle order; a group that does not fit stops the layout */
+  if (tid == 0) {
+    int nrow = 0, ng = 0, stop = 0;
+    for (int e = 0; e < m->neq && !stop; e++) {
+      int need = m->eq_type[e] == UR3E_EQ_CONNECT ? 3 : 1;
+      if (nrow + need > K_MAXEFC) { stop = 1; break; }
+      s.grp_type[ng] = m->eq_type[e] == UR3E_EQ_CONNECT ? G_CONNECT : G_JOINTEQ;
+      s.grp_id[ng] = e; s.grp_row[ng] = nrow; ng++; nrow += need;
+    }
+    for (int k = 0; k < pl->nfloss && !stop; k++) {
+      if (nrow + 1 > K_MAXEFC) { stop = 1; break; }
+      s.grp_type[ng] = G_FLOSS; s.grp_id[ng] = pl->floss_dof[k]; s.grp_row[ng] = nrow; ng++; nrow++;
+    }
+    for (int j = 0; j < m->njnt && !stop; j++) {
+      if (!m->jnt_limited[j]) continue;
+      if (m->jnt_type[j] != UR3E_JNT_HINGE && m->jnt_type[j] != UR3E_JNT_SLIDE) continue;
+      double q = s.qpos[m->jnt_qposadr[j]];
+      for (int side = -1; side <= 1; side += 2) {
+        double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
+        if (dist < m->jnt_margin[j]) {
+          if (nrow + 1 > K_MAXEFC) { stop = 1; break; }
+          s.grp_type[ng] = G_LIMIT; s.grp_id[ng] = 2 * j + (side + 1) / 2; s.grp_row[ng] = nrow; ng++; nrow++;
+        }
+      }
+    }
+    for (int c = 0; c < s.ncon && !stop; c++) {
+      if (m->cpair_condim[s.con_cpair[c]] != 3) continue;
+      if (nrow + 3 > K_MAXEFC) { stop = 1; break; }
+      s.grp_type[ng] = G_CONTACT; s.grp_id[ng] = c; s.grp_row[ng] = nrow; ng++; nrow += 3;
+    }
+    s.ngrp = ng;
+    s.nefc = nrow;
+  }
+  SYNC();
+  for (int g = tid; g < s.ngrp; g += NT) {
+    int type = s.grp_type[g], id = s.grp_id[g], r = s.grp_row[g];
+    if (type == G_CONNECT) {
+      int e = id;
+      int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      double p1[3], p2[3];
+      k_mat_vec3(p1, s.xmat[b1], m->eq_data[e]);
+      p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
+      k_mat_vec3(p2, s.xmat[b2], m->eq_data[e] + 3);
+      p2[0] += s.xpos[b2][0]; p2[1] += s.xpos[b2][1]; p2[2] += s.xpos[b2][2];
+      const double* c1 = s.subtree_com[m->body_rootid[b1]];
+      const double* c2 = s.subtree_com[m->body_rootid[b2]];
+      double o1[3] = {p1[0] - c1[0], p1[1] - c1[1], p1[2] - c1[2]};
+      double o2[3] = {p2[0] - c2[0], p2[1] - c2[1], p2[2] - c2[2]};
+      for (int v = 0; v < nv; v++) {
+        double j1[3], j2[3];
+        w_jacp_col(m, pl, s, b1, o1, v, j1);
+        w_jacp_col(m, pl, s, b2, o2, v, j2);
+        for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = j1[k] - j2[k];
+      }
+      double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      for (int k = 0; k < 3; k++) {
+        s.efc_type[r + k] = CN_EQUALITY; s.efc_id[r + k] = e; s.efc_floss[r + k] = 0;
+        w_row_impedance(m, s, r + k, m->eq_solref[e], m->eq_solimp[e], p1[k] - p2[k], 0, diag, 0);
+      }
+    } else if (type == G_JOINTEQ) {
+      int e = id;
+      int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
+      const double* c = m->eq_data[e];
+      int a1 = m->jnt_qposadr[j1];
+      double q1 = s.qpos[a1] - m->qpos0[a1];
+      double pos, dpoly = 0;
+      double diag = m->dof_invweight0[m->jnt_dofadr[j1]];
+      if (j2 >= 0) {
+        int a2 = m->jnt_qposadr[j2];
+        double q2 = s.qpos[a2] - m->qpos0[a2];
+        pos = q1 - (c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4]))));
+        dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
+        diag += m->dof_invweight0[m->jnt_dofadr[j2]];
+      } else {
+        pos = q1 - c[0];
+      }
+      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
+      s.efc_J[r][m->jnt_dofadr[j1]] = 1;
+      if (j2 >= 0) s.efc_J[r][m->jnt_dofadr[j2]] = -dpoly;
+      s.efc_type[r] = CN_EQUALITY; s.efc_id[r] = e; s.efc_floss[r] = 0;
+      w_row_impedance(m, s, r, m->eq_solref[e], m->eq_solimp[e], pos, 0, diag, 0);
+    } else if (type == G_FLOSS) {
+      int v0 = id;
+      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
+      s.efc_J[r][v0] = 1;
+      s.efc_type[r] = CN_FRICTION_DOF; s.efc_id[r] = v0; s.efc_floss[r] = m->dof_frictionloss[v0];
+      w_row_impedance(m, s, r, m->dof_solref[v0], m->dof_solimp[v0], 0, 0, m->dof_invweight0[v0], 1);
+    } else if (type == G_LIMIT) {
+      int j = id >> 1;
+      int side = (id & 1) ? 1 : -1;
+      double q = s.qpos[m->jnt_qposadr[j]];
+      double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
+      int dof = m->jnt_dofadr[j];
+      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
+      s.efc_J[r][dof] = -(double)side;
+      s.efc_type[r] = CN_LIMIT_JOINT; s.efc_id[r] = j; s.efc_floss[r] = 0;
+      w_row_impedance(m, s, r, m->jnt_solref[j], m->jnt_solimp[j], dist, m->jnt_margin[j], m->dof_invweight0[dof],
+                      0);
+    } else {
+      int c = id;
+      int p = s.con_cpair[c];
+      int b1 = m->geom_bodyid[s.con_geom1[c]], b2 = m->geom_bodyid[s.con_geom2[c]];
+      const double* pos = s.con_pos[c];
+      const double* c1 = s.subtree_com[m->body_rootid[b1]];
+      const double* c2 = s.subtree_com[m->body_rootid[b2]];
+      double o1[3] = {pos[0] - c1[0], pos[1] - c1[1], pos[2] - c1[2]};
+      double o2[3] = {pos[0] - c2[0], pos[1] - c2[1], pos[2] - c2[2]};
+      const double* fr = s.con_frame[c];
+      for (int v = 0; v < nv; v++) {
+        double j1[3], j2[3];
+        w_jacp_col(m, pl, s, b1, o1, v, j1);
+        w_jacp_col(m, pl, s, b2, o2, v, j2);
+        double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
+        for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = fr[3 * k] * dj0 + fr[3 * k + 1] * dj1 + fr[3 * k + 2] * dj2;
+      }
+      double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      double incl = m->cpair_margin[p] - m->cpair_gap[p];
+      s.con_efc[c] = r;
+      for (int k = 0; k < 3; k++) {
+        s.efc_type[r + k] = CN_CONTACT_ELLIPTIC; s.efc_id[r + k] = c; s.efc_floss[r + k] = 0;
+        w_row_impedance(m, s, r + k, m->cpair_solref[p], m->cpair_solimp[p], s.con_dist[c], incl, diag, k > 0);
+      }
+      double fr0 = m->cpair_friction[p][0];
+      s.efc_R[r + 1] = s.efc_R[r] / m->impratio;
+      s.con_mu[c] = fr0 * sqrt(s.efc_R[r + 1] / s.efc_R[r]);
+      /* condim 3: j = 1 only */
+      s.efc_R[r + 2] = s.efc_R[r + 1] * fr0 * fr0 / (m->cpair_friction[p][1] * m->cpair_friction[p][1]);
+    }
+  }
+  SYNC();
+  for (int i = tid; i < s.nefc; i += NT) s.efc_D[i] = 1.0 / s.efc_R[i];
+  SYNC();
+}
+
+/* ================================================================== */
+/* velocity stage                                                      */
+/* ================================================================== */
+template <int NT>
+__device__ static void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nb = m->nbody;
+  if (tid < 6) s.cvel[0][tid] = 0;
+  SYNC();
+  for (int lvl = 1; lvl <= pl->nlevel; lvl++) {
+    for (int i = tid; i < nb; i += NT) {
+      if (i == 0 || pl->body_depth[i] != lvl) continue;
+      double cv[6];
+      for (int k = 0; k < 6; k++) cv[k] = s.cvel[m->body_parentid[i]][k];
+      int bda = m->body_dofadr[i];
+      for (int j = 0; j < m->body_dofnum[i]; j++) {
+        int dof = bda + j;
+        int jt = m->jnt_type[m->dof_jntid[dof]];
+        if (jt == UR3E_JNT_FREE) {
+          for (int k = 0; k < 3; k++)
+            for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
+          double tmp[6] = {0, 0, 0, 0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+          for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+          for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
+          for (int r = 0; r < 6; r++) tmp[r] = 0;
+          for (int k = 3; k < 6; k++)
+            for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+          for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+          j += 5;
+        } else {
+          k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
+          for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
+        }
+      }
+      for (int k = 0; k < 6; k++) s.cvel[i][k] = cv[k];
+    }
+    SYNC();
+  }
+}
+
+template <int NT>
+__device__ static void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nb = m->nbody, nv = m->nv;
+  double (*cacc)[10] = s.u.body.b10;
+  double (*cfrc)[6] = s.u.body.b6;
+  if (tid == 0) {
+    cacc[0][0] = cacc[0][1] = cacc[0][2] = 0;
+    cacc[0][3] = -m->gravity[0]; cacc[0][4] = -m->gravity[1]; cacc[0][5] = -m->gravity[2];
+    for (int k = 0; k < 6; k++) cfrc[0][k] = 0;
+  }
+  SYNC();
+  for (int lvl = 1; lvl <= pl->nlevel; lvl++) {
+    for (int i = tid; i < nb; i += NT) {
+      if (i == 0 || pl->body_depth[i] != lvl) continue;
+      double tmp[6] = {0, 0, 0, 0, 0, 0};
+      int bda = m->body_dofadr[i];
+      for (int j = 0; j < m->body_dofnum[i]; j++)
+        for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+      int p = m->body_parentid[i];
+      for (int r = 0; r < 6; r++) cacc[i][r] = cacc[p][r] + tmp[r];
+    }
+    SYNC();
+  }
+  if (tid >= 1 && tid < nb) {
+    int i = tid;
+    double f1[6], f2[6], f3[6];
+    k_mul_inert_vec(f1, s.cinert[i], cacc[i]);
+    k_mul_inert_vec(f2, s.cinert[i], s.cvel[i]);
+    k_cross_force(f3, s.cvel[i], f2);
+    for (int r = 0; r < 6; r++) cfrc[i][r] = f1[r] + f3[r];
+  }
+  SYNC();
+  if (tid < 6) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m->body_parentid[i];
+      if (p > 0) cfrc[p][tid] += cfrc[i][tid];
+    }
+  }
+  SYNC();
+  if (tid < nv) {
+    int v = tid;
+    s.qfrc_bias[v] = k_dot6(s.cdof[v], cfrc[m->dof_bodyid[v]]);
+    /* passive: spring (per joint, one dof here) then damping */
+    double pf = 0;
+    int j = m->dof_jntid[v];
+    double k = m->jnt_stiffness[j];
+    if (k != 0 && (m->jnt_type[j] == UR3E_JNT_HINGE || m->jnt_type[j] == UR3E_JNT_SLIDE) && m->jnt_dofadr[j] == v) {
+      int a = m->jnt_qposadr[j];
+      pf = -k * (s.qpos[a] - m->qpos_spring[a]);
+    }
+    double b = m->dof_damping[v];
+    if (b != 0) pf -= b * s.qvel[v];
+    s.qfrc_passive[v] = pf;
+  }
+  for (int a = tid; a < m->nu; a += NT) {
+    double g = m->act_gear[a];
+    double vel = 0;
+    if (m->act_trntype[a] == UR3E_TRN_JOINT) {
+      int dof = m->jnt_dofadr[m->act_trnid[a]];
+      for (int v = 0; v < nv; v++) vel += (v == dof ? g : 0.0) * s.qvel[v];
+    } else {
+      int t = m->act_trnid[a];
+      for (int v = 0; v < nv; v++) {
+        double mom = 0;
+        for (int k = 0; k < m->ten_num[t]; k++)
+          if (m->ten_dof[t][k] == v) mom = m->ten_coef[t][k] * g;
+        vel += mom * s.qvel[v];
+      }
+    }
+    double ctrl = s.ctrl[a];
+    if (m->act_ctrllimited[a]) {
+      if (ctrl < m->act_ctrlrange[a][0]) ctrl = m->act_ctrlrange[a][0];
+      if (ctrl > m->act_ctrlrange[a][1]) ctrl = m->act_ctrlrange[a][1];
+    }
+    double f = m->act_gainprm[a][0] * ctrl;
+    if (m->act_biastype[a] == UR3E_BIAS_AFFINE)
+      f += m->act_biasprm[a][0] + m->act_biasprm[a][1] * s.actuator_length[a] + m->act_biasprm[a][2] * vel;
+    if (m->act_forcelimited[a]) {
+      if (f < m->act_forcerange[a][0]) f = m->act_forcerange[a][0];
+      if (f > m->act_forcerange[a][1]) f = m->act_forcerange[a][1];
+    }
+    s.act_force[a] = f;
+  }
+  SYNC();
+  if (tid < nv) {
+    int v = tid;
+    double sa = 0;
+    for (int a = 0; a < m->nu; a++) {
+      double mom;
+      if (m->act_trntype[a] == UR3E_TRN_JOINT) {
+        mom = (v == m->jnt_dofadr[m->act_trnid[a]]) ? m->act_gear[a] : 0.0;
+      } else {
+        int t = m->act_trnid[a];
+        mom = 0;
+        for (int k = 0; k < m->ten_num[t]; k++)
+          if (m->ten_dof[t][k] == v) mom = m->ten_coef[t][k] * m->act_gear[a];
+      }
+      sa += mom * s.act_force[a];
+    }
+    s.qfrc_smooth[v] = s.qfrc_passive[v] - s.qfrc_bias[v] + sa;
+  }
+  SYNC();
+}
+
+/* ================================================================== */
+/* Newton solver                                                       */
+/* ================================================================== */
+/* per-row force/state and cost contribution (rowflag: adds to the cost) */
+template <int NT>
+__device__ static void w_constraint_update(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nefc = s.nefc;
+  for (int i = tid; i < nefc; i += NT) {
+    int t = s.efc_type[i];
+    double D = s.efc_D[i], R = s.efc_R[i];
+    double jar = s.jar[i];
+    if (t == CN_EQUALITY) {
+      s.efc_force[i] = -D * jar;
+      s.u.row.F[i] = 0.5 * D * jar * jar; s.rowflag[i] = 1;
+      s.efc_state[i] = ST_QUADRATIC;
+    } else if (t == CN_FRICTION_DOF) {
+      double fl = s.efc_floss[i];
+      if (jar <= -R * fl) {
+        s.efc_force[i] = fl;
+        s.u.row.F[i] = -0.5 * R * fl * fl - fl * jar;
+        s.efc_state[i] = ST_LINEARNEG;
+      } else if (jar >= R * fl) {
+        s.efc_force[i] = -fl;
+        s.u.row.F[i] = -0.5 * R * fl * fl + fl * jar;
+        s.efc_state[i] = ST_LINEARPOS;
+      } else {
+        s.efc_force[i] = -D * jar;
+        s.u.row.F[i] = 0.5 * D * jar * jar;
+        s.efc_state[i] = ST_QUADRATIC;
+      }
+      s.rowflag[i] = 1;
+    } else if (t == CN_LIMIT_JOINT) {
+      if (jar >= 0) {
+        s.efc_force[i] = 0;
+        s.efc_state[i] = ST_SATISFIED;
+        s.rowflag[i] = 0;
+      } else {
+        s.efc_force[i] = -D * jar;
+        s.u.row.F[i] = 0.5 * D * jar * jar; s.rowflag[i] = 1;
+        s.efc_state[i] = ST_QUADRATIC;
+      }
+    } else {
+      int c = s.efc_id[i];
+      if (s.con_efc[c] != i) continue; /* cone handled at its first row */
+      int p = s.con_cpair[c];
+      const int dim = 3;
+      double mu = s.con_mu[c];
+      double U[3];
+      U[0] = s.jar[i] * mu;
+      for (int j = 1; j < dim; j++) U[j] = s.jar[i + j] * m->cpair_friction[p][j - 1];
+      double N = U[0];
+      double T2 = 0;
+      for (int j = 1; j < dim; j++) T2 += U[j] * U[j];
+      double T = sqrt(T2);
+      if (N >= mu * T || (T <= 0 && N >= 0)) {
+        for (int j = 0; j < dim; j++) {
+          s.efc_force[i + j] = 0;
+          s.efc_state[i + j] = ST_SATISFIED;
+          s.rowflag[i + j] = 0;
+        }
+      } else if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+        for (int j = 0; j < dim; j++) {
+          s.efc_force[i + j] = -s.efc_D[i + j] * s.jar[i + j];
+          s.u.row.F[i + j] = 0.5 * s.efc_D[i + j] * s.jar[i + j] * s.jar[i + j];
+          s.rowflag[i + j] = 1;
+          s.efc_state[i + j] = ST_QUADRATIC;
+        }
+      } else {
+        double Dm = s.efc_D[i] / (mu * mu * (1 + mu * mu));
+        double NT_ = N - mu * T;
+        s.u.row.F[i] = 0.5 * Dm * NT_ * NT_;
+        s.rowflag[i] = 1;
+        s.rowflag[i + 1] = 0;
+        s.rowflag[i + 2] = 0;
+        s.efc_force[i] = -Dm * NT_ * mu;
+        for (int j = 1; j < dim; j++) s.efc_force[i + j] = Dm * NT_ * mu * U[j] / T * m->cpair_friction[p][j - 1];
+        for (int j = 0; j < dim; j++) s.efc_state[i + j] = ST_CONE;
+      }
+    }
+  }
+  SYNC();
+}
+
+template <int NT>
+__device__ static void w_eval_state(KModel m, KS& s, const double* qacc) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  for (int i = tid; i < nv + s.nefc; i += NT) {
+    if (i < nv) {
+      double v = 0;
+      for (int j = 0; j < nv; j++) v += s.qM[i][j] * qacc[j];
+      s.Ma[i] = v;
+    } else {
+      int r = i - nv;
+      double v = 0;
+      for (int k = 0; k < nv; k++) v += s.efc_J[r][k] * qacc[k];
+      s.jar[r] = v - s.efc_aref[r];
+    }
+  }
+  SYNC();
+  w_constraint_update<NT>(m, s);
+  if (tid == 0) {
+    double g = 0;
+    for (int k = 0; k < nv; k++) g += (s.Ma[k] - s.qfrc_smooth[k]) * (qacc[k] - s.qacc_smooth[k]);
+    s.gauss = 0.5 * g;
+    double cost = 0;
+    for (int i = 0; i < s.nefc; i++)
+      if (s.rowflag[i]) cost += s.u.row.F[i];
+    s.cost = s.gauss + cost;
+  }
+  SYNC();
+}
+
+template <int NT>
+__device__ static void w_compute_grad(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  if (tid < nv) {
+    int k = tid;
+    double f = 0;
+    for (int i = 0; i < s.nefc; i++) f += s.efc_J[i][k] * s.efc_force[i];
+    s.qfrc_constraint[k] = f;
+    s.grad[k] = s.Ma[k] - s.qfrc_smooth[k] - f;
+  }
+  SYNC();
+}
+
+template <int NT>
+__device__ static void w_hessian_factor(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  /* cone Hessians (middle zone), one lane per contact */
+  for (int c = tid; c < s.ncon; c += NT) {
+    int i = s.con_efc[c];
+    if (i < 0 || s.efc_state[i] != ST_CONE) continue;
+    int p = s.con_cpair[c];
+    const int dim = 3;
+    double mu = s.con_mu[c];
+    double U[3], sc[3];
+    sc[0] = mu;
+    U[0] = s.jar[i] * mu;
+    for (int j = 1; j < dim; j++) {
+      sc[j] = m->cpair_friction[p][j - 1];
+      U[j] = s.jar[i + j] * sc[j];
+    }
+    double T2 = 0;
+    for (int j = 1; j < dim; j++) T2 += U[j] * U[j];
+    double T = sqrt(T2);
+    double N = U[0];
+    double Dm = s.efc_D[i] / (mu * mu * (1 + mu * mu));
+    double Hc[3][3];
+    Hc[0][0] = 1;
+    for (int j = 1; j < dim; j++) {
+      Hc[0][j] = -mu * U[j] / T;
+      Hc[j][0] = Hc[0][j];
+    }
+    double muNT = mu * N / T;
+    for (int j = 1; j < dim; j++)
+      for (int k = 1; k < dim; k++) Hc[j][k] = (j == k ? mu * mu - muNT : 0.0) + muNT * U[j] * U[k] / T2;
+    for (int j = 0; j < dim; j++)
+      for (int k = 0; k < dim; k++) s.con_Hc[c][3 * j + k] = Hc[j][k] * Dm * sc[j] * sc[k];
+  }
+  SYNC();
+  /* H = M + J' D J + cone blocks, lower triangle, one lane per element, rows in oracle order */
+  const int nel = nv * (nv + 1) / 2;
+  for (int e = tid; e < nel; e += NT) {
+    int r = 0, rem = e;
+    while (rem > r) { rem -= r + 1; r++; }
+    int c = rem;
+    double h = s.qM[r][c];
+    for (int i = 0; i < s.nefc; i++) {
+      int st = s.efc_state[i];
+      if (st == ST_QUADRATIC) {
+        double jr = s.efc_J[i][r];
+        if (jr == 0) continue;
+        double djr = s.efc_D[i] * jr;
+        h += djr * s.efc_J[i][c];
+      } else if (st == ST_CONE && s.efc_type[i] == CN_CONTACT_ELLIPTIC) {
+        int ci = s.efc_id[i];
+        if (s.con_efc[ci] != i) continue;
+        const double* Hc = s.con_Hc[ci];
+        double t[3];
+        for (int j = 0; j < 3; j++) {
+          double acc = 0;
+          for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[i + k][r];
+          t[j] = acc;
+        }
+        double acc = 0;
+        for (int j = 0; j < 3; j++) acc += s.efc_J[i + j][c] * t[j];
+        h += acc;
+      }
+    }
+    s.H[r][c] = h;
+  }
+  SYNC();
+  /* Cholesky H = L L' (lower), column by column */
+  for (int j = 0; j < nv; j++) {
+    if (tid == 0) {
+      double sum = s.H[j][j];
+      for (int k = 0; k < j; k++) sum -= s.H[j][k] * s.H[j][k];
+      if (sum < K_MINVAL) sum = K_MINVAL;
+      s.H[j][j] = sqrt(sum);
+    }
+    SYNC();
+    double ljj = s.H[j][j];
+    for (int i = j + 1 + tid; i < nv; i += NT) {
+      double v = s.H[i][j];
+      for (int k = 0; k < j; k++) v -= s.H[i][k] * s.H[j][k];
+      s.H[i][j] = v / ljj;
+    }
+    SYNC();
+  }
+}
+
+/* x = H^-1 b by column sweeps (oracle order: forward k ascending, back k descending) */
+template <int NT>
+__device__ static void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  if (tid < nv) s.tmpv[tid] = b[tid];
+  SYNC();
+  for (int k = 0; k < nv; k++) {
+    if (tid == 0) x[k] = s.tmpv[k] / s.H[k][k];
+    SYNC();
+    if (tid > k && tid < nv) s.tmpv[tid] -= s.H[tid][k] * x[k];
+    SYNC();
+  }
+  if (tid < nv) s.tmpv[tid] = x[tid];
+  SYNC();
+  for (int i = nv - 1; i >= 0; i--) {
+    if (tid == 0) x[i] = s.tmpv[i] / s.H[i][i];
+    SYNC();
+    if (tid < i) s.tmpv[tid] -= s.H[i][tid] * x[i];
+    SYNC();
+  }
+}
+
+/* line-search 1-D evaluation at step a: per-row contributions + ordered sums on lane 0 */
+template <int NT>
+__device__ static void w_ls_eval(KModel m, KS& s, double a) {
+  const int tid = threadIdx.x;
+  const int nefc = s.nefc;
+  for (int i = tid; i < nefc; i += NT) {
+    int t = s.efc_type[i];
+    double D = s.efc_D[i], R = s.efc_R[i];
+    double x = s.jar[i] + a * s.Jv[i];
+    double v = s.Jv[i];
+    double F = 0, dF = 0, d2F = 0;
+    int flag = 0; /* 1: F,dF,d2F; 2: F,dF only */
+    if (t == CN_EQUALITY) {
+      F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
+    } else if (t == CN_FRICTION_DOF) {
+      double fl = s.efc_floss[i];
+      if (x <= -R * fl) { F = -0.5 * R * fl * fl - fl * x; dF = -fl * v; flag = 2; }
+      else if (x >= R * fl) { F = -0.5 * R * fl * fl + fl * x; dF = fl * v; flag = 2; }
+      else { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+    } else if (t == CN_LIMIT_JOINT) {
+      if (x < 0) { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+    } else {
+      int c = s.efc_id[i];
+      if (s.con_efc[c] != i) continue;
+      int p = s.con_cpair[c];
+      const int dim = 3;
+      double mu = s.con_mu[c];
+      double U[3], V[3];
+      U[0] = (s.jar[i] + a * s.Jv[i]) * mu;
+      V[0] = s.Jv[i] * mu;
+      for (int j = 1; j < dim; j++) {
+        U[j] = (s.jar[i + j] + a * s.Jv[i + j]) * m->cpair_friction[p][j - 1];
+        V[j] = s.Jv[i + j] * m->cpair_friction[p][j - 1];
+      }
+      double N = U[0];
+      double T2 = 0;
+      for (int j = 1; j < dim; j++) T2 += U[j] * U[j];
+      double T = sqrt(T2);
+      s.rowflag[i + 1] = 0;
+      s.rowflag[i + 2] = 0;
+      if (N >= mu * T || (T <= 0 && N >= 0)) {
+      } else if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+        for (int j = 0; j < dim; j++) {
+          double xj = s.jar[i + j] + a * s.Jv[i + j];
+          double vj = s.Jv[i + j];
+          double Dj = s.efc_D[i + j];
+          s.u.row.F[i + j] = 0.5 * Dj * xj * xj;
+          s.u.row.dF[i + j] = Dj * xj * vj;
+          s.u.row.d2F[i + j] = Dj * vj * vj;
+          s.rowflag[i + j] = 1;
+        }
+        continue;
+      } else {
+        double Dm = s.efc_D[i] / (mu * mu * (1 + mu * mu));
+        double UV = 0, VV = 0;
+        for (int j = 1; j < dim; j++) { UV += U[j] * V[j]; VV += V[j] * V[j]; }
+        double NT_ = N - mu * T;
+        double dNT = V[0] - mu * UV / T;
+        double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
+        F = 0.5 * Dm * NT_ * NT_;
+        dF = Dm * NT_ * dNT;
+        d2F = Dm * (dNT * dNT + NT_ * d2NT);
+        flag = 1;
+      }
+    }
+    s.u.row.F[i] = F; s.u.row.dF[i] = dF; s.u.row.d2F[i] = d2F;
+    s.rowflag[i] = flag;
+  }
+  SYNC();
+  if (tid == 0) {
+    double F = s.gauss + a * s.g1 + 0.5 * a * a * s.g2;
+    double dF = s.g1 + a * s.g2;
+    double d2F = s.g2;
+    for (int i = 0; i < nefc; i++) {
+      int f = s.rowflag[i];
+      if (f) {
+        F += s.u.row.F[i];
+        dF += s.u.row.dF[i];
+        if (f == 1) d2F += s.u.row.d2F[i];
+      }
+    }
+    s.lsF = F; s.lsdF = dF; s.lsd2F = d2F;
+  }
+  SYNC();
+}
+
+template <int NT>
+__device__ static double w_line_search(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  if (tid == 0) {
+    double sn = 0;
+    for (int k = 0; k < nv; k++) sn += s.search[k] * s.search[k];
+    s.sred = sqrt(sn);
+  }
+  for (int i = tid; i < nv + s.nefc; i += NT) {
+    if (i < nv) {
+      double v = 0;
+      for (int j = 0; j < nv; j++) v += s.qM[i][j] * s.search[j];
+      s.Mv[i] = v;
+    } else {
+      int r = i - nv;
+      double v = 0;
+      for (int k = 0; k < nv; k++) v += s.efc_J[r][k] * s.search[k];
+      s.Jv[r] = v;
+    }
+  }
+  SYNC();
+  double snorm = s.sred;
+  if (snorm < K_MINVAL) return 0;
+  if (tid == 0) {
+    double g1 = 0, g2 = 0;
+    for (int k = 0; k < nv; k++) {
+      g1 += s.search[k] * (s.Ma[k] - s.qfrc_smooth[k]);
+      g2 += s.search[k] * s.Mv[k];
+    }
+    s.g1 = g1; s.g2 = g2;
+  }
+  SYNC();
+  double gtol = m->tolerance * m->ls_tolerance * snorm / s.scale;
+  w_ls_eval<NT>(m, s, 0.0);
+  double f0 = s.lsF, d0 = s.lsdF, h0 = s.lsd2F;
+  if (d0 >= 0) return 0;
+  double lo = 0.0, dlo = d0, hlo = h0;
+  double hi = -1.0, dhi = 0, hhi = 0;
+  double bestA = 0.0, bestF = f0;
+  double a = -d0 / h0;
+  for (int it = 0; it < m->ls_iterations; it++) {
+    w_ls_eval<NT>(m, s, a);
+    double f = s.lsF, df = s.lsdF, d2f = s.lsd2F;
+    if (f < bestF) { bestF = f; bestA = a; }
+    if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
+    if (df < 0) { lo = a; dlo = df; hlo = d2f; }
+    else { hi = a; dhi = df; hhi = d2f; }
+    double na;
+    if (hi < 0) {
+      na = a - df / d2f;
+      if (!(na > a)) na = 2 * a;
+    } else {
+      double c1 = lo - dlo / hlo;
+      double c2 = hi - dhi / hhi;
+      if (c1 > lo && c1 < hi) na = c1;
+      else if (c2 > lo && c2 < hi) na = c2;
+      else na = 0.5 * (lo + hi);
+    }
+    a = na;
+  }
+  return bestA;
+}
+
+template <int NT>
+__device__ static void w_solve_newton(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  if (s.nefc == 0) {
+    if (tid < nv) { s.qacc[tid] = s.qacc_smooth[tid]; s.qfrc_constraint[tid] = 0; }
+    SYNC();
+    return;
+  }
+  if (tid == 0) s.scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  if (tid < nv) s.qacc[tid] = s.warm[tid];
+  SYNC();
+  w_eval_state<NT>(m, s, s.qacc);
+  double cost_ws = s.cost;
+  w_eval_state<NT>(m, s, s.qacc_smooth);
+  double cost_sm = s.cost;
+  if (cost_ws > cost_sm) {
+    if (tid < nv) s.qacc[tid] = s.qacc_smooth[tid];
+    SYNC();
+  } else {
+    w_eval_state<NT>(m, s, s.qacc);
+  }
+  w_compute_grad<NT>(m, s);
+  w_hessian_factor<NT>(m, s);
+  w_hessian_solve<NT>(m, s, s.xv, s.grad);
+  if (tid < nv) s.search[tid] = -s.xv[tid];
+  SYNC();
+  for (int iter = 0; iter < m->iterations; iter++) {
+    double alpha = w_line_search<NT>(m, s);
+    if (alpha == 0) break;
+    if (tid < nv) s.qacc[tid] += alpha * s.search[tid];
+    SYNC();
+    double oldcost = s.cost;
+    w_eval_state<NT>(m, s, s.qacc);
+    w_compute_grad<NT>(m, s);
+    if (tid == 0) {
+      double gn = 0;
+      for (int k = 0; k < nv; k++) gn += s.grad[k] * s.grad[k];
+      s.sred = gn;
+    }
+    SYNC();
+    double improvement = s.scale * (oldcost - s.cost);
+    double gradient = s.scale * sqrt(s.sred);
+    if (improvement < m->tolerance || gradient < m->tolerance) break;
+    w_hessian_factor<NT>(m, s);
+    w_hessian_solve<NT>(m, s, s.xv, s.grad);
+    if (tid < nv) s.search[tid] = -s.xv[tid];
+    SYNC();
+  }
+}
+
+/* ================================================================== */
+/* forward / step                                                      */
+/* ================================================================== */
+template <int NT>
+__device__ static void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = m->nv;
+  w_kinematics<NT>(m, pl, s);
+  w_com_pos<NT>(m, pl, s);
+  w_crb<NT>(m, s);
+  for (int e = tid; e < nv * nv; e += NT) s.qLD[e / nv][e % nv] = s.qM[e / nv][e % nv];
+  SYNC();
+  w_factor_tree<NT>(m, pl, s.qLD, s.LDinv, s.tmpv);
+  w_collision<NT>(m, s);
+  w_make_constraint<NT>(m, pl, s);
+  w_com_vel<NT>(m, pl, s);
+  w_rne_passive<NT>(m, pl, s);
+  w_solve_tree<NT>(m, pl, s.qLD, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+  w_solve_newton<NT>(m, s);
+}
+
+template <int NT>
+__device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nq = m->nq, nv = m->nv;
+  if (tid == 0) {
+    int bad = 0;
+    for (int k = 0; k < nq; k++) bad |= k_is_bad(s.qpos[k]);
+    for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qvel[k]);
+    s.flag = bad;
+  }
+  SYNC();
+  if (s.flag) {
+    if (tid < nq) s.qpos[tid] = m->qpos0[tid];
+    if (tid < nv) { s.qvel[tid] = 0; s.warm[tid] = 0; }
+    if (tid == 0) s.nwarn++;
+    SYNC();
+  }
+  w_forward<NT>(m, pl, s);
+  if (tid == 0) {
+    int bad = 0;
+    for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qacc[k]);
+    s.flag = bad;
+  }
+  SYNC();
+  if (s.flag) {
+    if (tid < nq) s.qpos[tid] = m->qpos0[tid];
+    if (tid < nv) { s.qvel[tid] = 0; s.warm[tid] = 0; }
+    if (tid == 0) s.nwarn++;
+    SYNC();
+    w_forward<NT>(m, pl, s);
+  }
+  /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
+  int damped = 0;
+  for (int k = 0; k < nv; k++) damped |= m->dof_damping[k] > 0;
+  if (damped) {
+    for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
+    SYNC();
+    if (tid < nv) {
+      s.H[tid][tid] += m->timestep * m->dof_damping[tid];
+      s.fv[tid] = s.qfrc_smooth[tid] + s.qfrc_constraint[tid];
+    }
+    SYNC();
+    w_factor_tree<NT>(m, pl, s.H, s.grad, s.tmpv);
+    w_solve_tree<NT>(m, pl, s.H, s.grad, s.xv, s.fv);
+  } else {
+    if (tid < nv) s.xv[tid] = s.qacc[tid];
+    SYNC();
+  }
+  double h = m->timestep;
+  if (tid < nv) s.qvel[tid] += h * s.xv[tid];
+  SYNC();
+  for (int j = tid; j < m->njnt; j += NT) {
+    int a = m->jnt_qposadr[j], v = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == UR3E_JNT_FREE) {
+      s.qpos[a] += h * s.qvel[v];
+      s.qpos[a + 1] += h * s.qvel[v + 1];
+      s.qpos[a + 2] += h * s.qvel[v + 2];
+      double w[3] = {s.qvel[v + 3], s.qvel[v + 4], s.qvel[v + 5]};
+      double ang = h * k_normalize3(w);
+      double qr[4];
+      k_axis_angle_quat(qr, w, ang);
+      double q[4] = {s.qpos[a + 3], s.qpos[a + 4], s.qpos[a + 5], s.qpos[a + 6]};
+      k_normalize4(q);
+      k_mul_quat(q, q, qr);
+      s.qpos[a + 3] = q[0]; s.qpos[a + 4] = q[1]; s.qpos[a + 5] = q[2]; s.qpos[a + 6] = q[3];
+    } else {
+      s.qpos[a] += h * s.qvel[v];
+    }
+  }
+  if (tid < nv) s.warm[tid] = s.qacc[tid];
+  SYNC();
+}
+
+#endif /* UR3E_WAVE_H */
