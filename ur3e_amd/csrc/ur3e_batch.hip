@@ -1009,6 +1009,24 @@ extern "C" int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, 
   return UR3E_OK;
 }
 
+/* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */
+extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {
+#ifdef UR3E_STAGE_TIMING
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(cycles, HIP_SYMBOL(ur3e_stage_cycles), sizeof(unsigned long long) * 32));
+  HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(ur3e_stage_calls), sizeof(unsigned long long) * 32));
+  if (reset) {
+    unsigned long long z[32] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_cycles), z, sizeof(z)));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_calls), z, sizeof(z)));
+  }
+  return UR3E_OK;
+#else
+  (void)cycles; (void)calls; (void)reset;
+  return fail(UR3E_EINVAL, "library built without -DUR3E_STAGE_TIMING");
+#endif
+}
+
 extern "C" int ur3e_batch_num_envs(const ur3e_batch_t* b) { return b ? b->n : 0; }
 extern "C" int ur3e_batch_nq(const ur3e_batch_t* b) { return b ? b->host_model.nq : 0; }
 extern "C" int ur3e_batch_nv(const ur3e_batch_t* b) { return b ? b->host_model.nv : 0; }

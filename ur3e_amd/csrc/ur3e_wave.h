@@ -59,7 +59,9 @@ struct KS {
   double subtree_com[K_NB][3], cinert[K_NB][10], cdof[K_NV][6];
   double cvel[K_NB][6], cdof_dot[K_NV][6];
   double actuator_length[K_NU], act_force[K_NU];
-  double qM[K_NV][K_NV], qLD[K_NV][K_NV], LDinv[K_NV], H[K_NV][K_NV];
+  double qM[K_NV][K_NV], LDinv[K_NV];
+  double H[K_NV][K_NV]; /* Newton Hessian; also holds the tree factor of M before Newton (qLD) */
+  double qloc[K_NJ][4];
   /* vectors */
   double qfrc_bias[K_NV], qfrc_passive[K_NV], qfrc_smooth[K_NV], qacc_smooth[K_NV], qacc[K_NV];
   double qfrc_constraint[K_NV], Ma[K_NV], grad[K_NV], search[K_NV], Mv[K_NV], xv[K_NV], fv[K_NV];
@@ -83,14 +85,54 @@ struct KS {
   double efc_J[K_MAXEFC][K_NV];
   double efc_R[K_MAXEFC], efc_D[K_MAXEFC], efc_aref[K_MAXEFC], efc_floss[K_MAXEFC];
   double efc_force[K_MAXEFC], jar[K_MAXEFC], Jv[K_MAXEFC];
-  int efc_type[K_MAXEFC], efc_id[K_MAXEFC], efc_state[K_MAXEFC], rowflag[K_MAXEFC];
+  int efc_type[K_MAXEFC], efc_id[K_MAXEFC], efc_state[K_MAXEFC], rowflag[K_MAXEFC], efc_grp[K_MAXEFC];
   int grp_type[W_MAXGRP], grp_id[W_MAXGRP], grp_row[W_MAXGRP];
   /* scalars */
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
   int ncon, nefc, ngrp, nwarn, flag;
+  unsigned long long tlast;
 };
 
-#define SYNC() __syncthreads()
+/* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
+   wave's LDS instructions issue and complete in program order, so cross-lane LDS hand-offs only
+   need a compiler fence (no s_barrier, no workgroup fence); with NT == 128 the two waves need a
+   real workgroup barrier. */
+template <int NT>
+__device__ __forceinline__ void wsync() {
+  if constexpr (NT == 64) {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
+#define SYNC() wsync<NT>()
+
+/* diagnostic build only (-DUR3E_STAGE_TIMING): per-stage shader-clock cycles, lane 0 of every env */
+#ifdef UR3E_STAGE_TIMING
+__device__ unsigned long long ur3e_stage_cycles[32];
+__device__ unsigned long long ur3e_stage_calls[32];
+#define WT(k)                                                           \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      unsigned long long _t = __builtin_amdgcn_s_memtime();            \
+      atomicAdd(&ur3e_stage_cycles[k], _t - s.tlast);                   \
+      atomicAdd(&ur3e_stage_calls[k], 1ull);                            \
+      s.tlast = _t;                                                     \
+    }                                                                   \
+  } while (0)
+#define WT_START()                                                      \
+  do {                                                                  \
+    if (threadIdx.x == 0) s.tlast = __builtin_amdgcn_s_memtime();       \
+  } while (0)
+#else
+#define WT(k) \
+  do {        \
+  } while (0)
+#define WT_START() \
+  do {             \
+  } while (0)
+#endif
 
 /* ================================================================== */
 /* kinematics (level-parallel over bodies)                             */
@@ -102,6 +144,12 @@ __device__ static void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& 
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
     k_quat2mat(s.xmat[0], s.xquat[0]);
+  }
+  /* hinge rotations do not depend on the parent: all joints at once */
+  for (int j = tid; j < m->njnt; j += NT) {
+    if (m->jnt_type[j] == UR3E_JNT_FREE) continue;
+    int a = m->jnt_qposadr[j];
+    k_axis_angle_quat(s.qloc[j], m->jnt_axis[j], s.qpos[a] - m->qpos0[a]);
   }
   SYNC();
   const int nb = m->nbody;
@@ -125,13 +173,11 @@ __device__ static void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& 
         k_mul_quat(xquat, s.xquat[pid], m->body_quat[i]);
         for (int k = 0; k < m->body_jntnum[i]; k++) {
           int j = jfirst + k;
-          double xaxis[3], xanchor[3], qloc[4], vec[3];
+          double xaxis[3], xanchor[3], vec[3];
           k_rot_vec_quat(xaxis, m->jnt_axis[j], xquat);
           k_rot_vec_quat(xanchor, m->jnt_pos[j], xquat);
           xanchor[0] += xpos[0]; xanchor[1] += xpos[1]; xanchor[2] += xpos[2];
-          int a = m->jnt_qposadr[j];
-          k_axis_angle_quat(qloc, m->jnt_axis[j], s.qpos[a] - m->qpos0[a]);
-          k_mul_quat(xquat, xquat, qloc);
+          k_mul_quat(xquat, xquat, s.qloc[j]);
           k_rot_vec_quat(vec, m->jnt_pos[j], xquat);
           xpos[0] = xanchor[0] - vec[0]; xpos[1] = xanchor[1] - vec[1]; xpos[2] = xanchor[2] - vec[2];
           for (int c = 0; c < 3; c++) { s.xanchor[j][c] = xanchor[c]; s.xaxis[j][c] = xaxis[c]; }
@@ -494,8 +540,22 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
     s.nefc = nrow;
   }
   SYNC();
-  for (int g = tid; g < s.ngrp; g += NT) {
+  /* phase A: Jacobian entries, one lane per (group, dof) */
+  const int nitem = s.ngrp * nv;
+  for (int it = tid; it < nitem; it += NT) {
+    int g = it / nv, v = it % nv;
     int type = s.grp_type[g], id = s.grp_id[g], r = s.grp_row[g];
+    int nrow = (type == G_CONNECT || type == G_CONTACT) ? 3 : 1;
+    if (v == 0) {
+      int ct = type == G_CONNECT || type == G_JOINTEQ ? CN_EQUALITY
+             : type == G_FLOSS ? CN_FRICTION_DOF : type == G_LIMIT ? CN_LIMIT_JOINT : CN_CONTACT_ELLIPTIC;
+      int cid = type == G_LIMIT ? (id >> 1) : id;
+      for (int k = 0; k < nrow; k++) {
+        s.efc_type[r + k] = ct; s.efc_id[r + k] = cid; s.efc_grp[r + k] = g;
+        s.efc_floss[r + k] = type == G_FLOSS ? m->dof_frictionloss[id] : 0.0;
+      }
+      if (type == G_CONTACT) s.con_efc[id] = r;
+    }
     if (type == G_CONNECT) {
       int e = id;
       int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
@@ -508,59 +568,31 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
       const double* c2 = s.subtree_com[m->body_rootid[b2]];
       double o1[3] = {p1[0] - c1[0], p1[1] - c1[1], p1[2] - c1[2]};
       double o2[3] = {p2[0] - c2[0], p2[1] - c2[1], p2[2] - c2[2]};
-      for (int v = 0; v < nv; v++) {
-        double j1[3], j2[3];
-        w_jacp_col(m, pl, s, b1, o1, v, j1);
-        w_jacp_col(m, pl, s, b2, o2, v, j2);
-        for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = j1[k] - j2[k];
-      }
-      double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
-      for (int k = 0; k < 3; k++) {
-        s.efc_type[r + k] = CN_EQUALITY; s.efc_id[r + k] = e; s.efc_floss[r + k] = 0;
-        w_row_impedance(m, s, r + k, m->eq_solref[e], m->eq_solimp[e], p1[k] - p2[k], 0, diag, 0);
-      }
+      double j1[3], j2[3];
+      w_jacp_col(m, pl, s, b1, o1, v, j1);
+      w_jacp_col(m, pl, s, b2, o2, v, j2);
+      for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = j1[k] - j2[k];
     } else if (type == G_JOINTEQ) {
       int e = id;
       int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
-      const double* c = m->eq_data[e];
-      int a1 = m->jnt_qposadr[j1];
-      double q1 = s.qpos[a1] - m->qpos0[a1];
-      double pos, dpoly = 0;
-      double diag = m->dof_invweight0[m->jnt_dofadr[j1]];
-      if (j2 >= 0) {
+      double val = 0;
+      if (v == m->jnt_dofadr[j1]) val = 1;
+      if (j2 >= 0 && v == m->jnt_dofadr[j2]) {
+        const double* c = m->eq_data[e];
         int a2 = m->jnt_qposadr[j2];
         double q2 = s.qpos[a2] - m->qpos0[a2];
-        pos = q1 - (c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4]))));
-        dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
-        diag += m->dof_invweight0[m->jnt_dofadr[j2]];
-      } else {
-        pos = q1 - c[0];
+        double dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
+        val = -dpoly;
       }
-      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
-      s.efc_J[r][m->jnt_dofadr[j1]] = 1;
-      if (j2 >= 0) s.efc_J[r][m->jnt_dofadr[j2]] = -dpoly;
-      s.efc_type[r] = CN_EQUALITY; s.efc_id[r] = e; s.efc_floss[r] = 0;
-      w_row_impedance(m, s, r, m->eq_solref[e], m->eq_solimp[e], pos, 0, diag, 0);
+      s.efc_J[r][v] = val;
     } else if (type == G_FLOSS) {
-      int v0 = id;
-      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
-      s.efc_J[r][v0] = 1;
-      s.efc_type[r] = CN_FRICTION_DOF; s.efc_id[r] = v0; s.efc_floss[r] = m->dof_frictionloss[v0];
-      w_row_impedance(m, s, r, m->dof_solref[v0], m->dof_solimp[v0], 0, 0, m->dof_invweight0[v0], 1);
+      s.efc_J[r][v] = v == id ? 1.0 : 0.0;
     } else if (type == G_LIMIT) {
       int j = id >> 1;
       int side = (id & 1) ? 1 : -1;
-      double q = s.qpos[m->jnt_qposadr[j]];
-      double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
-      int dof = m->jnt_dofadr[j];
-      for (int v = 0; v < nv; v++) s.efc_J[r][v] = 0;
-      s.efc_J[r][dof] = -(double)side;
-      s.efc_type[r] = CN_LIMIT_JOINT; s.efc_id[r] = j; s.efc_floss[r] = 0;
-      w_row_impedance(m, s, r, m->jnt_solref[j], m->jnt_solimp[j], dist, m->jnt_margin[j], m->dof_invweight0[dof],
-                      0);
+      s.efc_J[r][v] = v == m->jnt_dofadr[j] ? -(double)side : 0.0;
     } else {
       int c = id;
-      int p = s.con_cpair[c];
       int b1 = m->geom_bodyid[s.con_geom1[c]], b2 = m->geom_bodyid[s.con_geom2[c]];
       const double* pos = s.con_pos[c];
       const double* c1 = s.subtree_com[m->body_rootid[b1]];
@@ -568,26 +600,74 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
       double o1[3] = {pos[0] - c1[0], pos[1] - c1[1], pos[2] - c1[2]};
       double o2[3] = {pos[0] - c2[0], pos[1] - c2[1], pos[2] - c2[2]};
       const double* fr = s.con_frame[c];
-      for (int v = 0; v < nv; v++) {
-        double j1[3], j2[3];
-        w_jacp_col(m, pl, s, b1, o1, v, j1);
-        w_jacp_col(m, pl, s, b2, o2, v, j2);
-        double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
-        for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = fr[3 * k] * dj0 + fr[3 * k + 1] * dj1 + fr[3 * k + 2] * dj2;
+      double j1[3], j2[3];
+      w_jacp_col(m, pl, s, b1, o1, v, j1);
+      w_jacp_col(m, pl, s, b2, o2, v, j2);
+      double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
+      for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = fr[3 * k] * dj0 + fr[3 * k + 1] * dj1 + fr[3 * k + 2] * dj2;
+    }
+  }
+  SYNC();
+  /* phase B: reference acceleration and regulariser, one lane per row */
+  for (int r = tid; r < s.nefc; r += NT) {
+    int g = s.efc_grp[r];
+    int type = s.grp_type[g], id = s.grp_id[g];
+    int k = r - s.grp_row[g];
+    if (type == G_CONNECT) {
+      int e = id;
+      int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      double p1[3], p2[3];
+      k_mat_vec3(p1, s.xmat[b1], m->eq_data[e]);
+      p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
+      k_mat_vec3(p2, s.xmat[b2], m->eq_data[e] + 3);
+      p2[0] += s.xpos[b2][0]; p2[1] += s.xpos[b2][1]; p2[2] += s.xpos[b2][2];
+      double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      w_row_impedance(m, s, r, m->eq_solref[e], m->eq_solimp[e], p1[k] - p2[k], 0, diag, 0);
+    } else if (type == G_JOINTEQ) {
+      int e = id;
+      int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
+      const double* c = m->eq_data[e];
+      int a1 = m->jnt_qposadr[j1];
+      double q1 = s.qpos[a1] - m->qpos0[a1];
+      double pos;
+      double diag = m->dof_invweight0[m->jnt_dofadr[j1]];
+      if (j2 >= 0) {
+        int a2 = m->jnt_qposadr[j2];
+        double q2 = s.qpos[a2] - m->qpos0[a2];
+        pos = q1 - (c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4]))));
+        diag += m->dof_invweight0[m->jnt_dofadr[j2]];
+      } else {
+        pos = q1 - c[0];
       }
+      w_row_impedance(m, s, r, m->eq_solref[e], m->eq_solimp[e], pos, 0, diag, 0);
+    } else if (type == G_FLOSS) {
+      w_row_impedance(m, s, r, m->dof_solref[id], m->dof_solimp[id], 0, 0, m->dof_invweight0[id], 1);
+    } else if (type == G_LIMIT) {
+      int j = id >> 1;
+      int side = (id & 1) ? 1 : -1;
+      double q = s.qpos[m->jnt_qposadr[j]];
+      double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
+      w_row_impedance(m, s, r, m->jnt_solref[j], m->jnt_solimp[j], dist, m->jnt_margin[j],
+                      m->dof_invweight0[m->jnt_dofadr[j]], 0);
+    } else {
+      int c = id;
+      int p = s.con_cpair[c];
+      int b1 = m->geom_bodyid[s.con_geom1[c]], b2 = m->geom_bodyid[s.con_geom2[c]];
       double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
       double incl = m->cpair_margin[p] - m->cpair_gap[p];
-      s.con_efc[c] = r;
-      for (int k = 0; k < 3; k++) {
-        s.efc_type[r + k] = CN_CONTACT_ELLIPTIC; s.efc_id[r + k] = c; s.efc_floss[r + k] = 0;
-        w_row_impedance(m, s, r + k, m->cpair_solref[p], m->cpair_solimp[p], s.con_dist[c], incl, diag, k > 0);
-      }
-      double fr0 = m->cpair_friction[p][0];
-      s.efc_R[r + 1] = s.efc_R[r] / m->impratio;
-      s.con_mu[c] = fr0 * sqrt(s.efc_R[r + 1] / s.efc_R[r]);
-      /* condim 3: j = 1 only */
-      s.efc_R[r + 2] = s.efc_R[r + 1] * fr0 * fr0 / (m->cpair_friction[p][1] * m->cpair_friction[p][1]);
+      w_row_impedance(m, s, r, m->cpair_solref[p], m->cpair_solimp[p], s.con_dist[c], incl, diag, k > 0);
     }
+  }
+  SYNC();
+  /* phase C: elliptic regularisation per contact */
+  for (int g = tid; g < s.ngrp; g += NT) {
+    if (s.grp_type[g] != G_CONTACT) continue;
+    int c = s.grp_id[g], r = s.grp_row[g];
+    int p = s.con_cpair[c];
+    double fr0 = m->cpair_friction[p][0];
+    s.efc_R[r + 1] = s.efc_R[r] / m->impratio;
+    s.con_mu[c] = fr0 * sqrt(s.efc_R[r + 1] / s.efc_R[r]);
+    s.efc_R[r + 2] = s.efc_R[r + 1] * fr0 * fr0 / (m->cpair_friction[p][1] * m->cpair_friction[p][1]);
   }
   SYNC();
   for (int i = tid; i < s.nefc; i += NT) s.efc_D[i] = 1.0 / s.efc_R[i];
@@ -843,14 +923,21 @@ __device__ static void w_eval_state(KModel m, KS& s, const double* qacc) {
   }
   SYNC();
   w_constraint_update<NT>(m, s);
+  /* lane 0: Gauss term (k order), lane 1: constraint cost (row order) -- one loop, two data streams */
+  if (tid < 2) {
+    double acc = 0;
+    int len = tid == 0 ? nv : s.nefc;
+    for (int i = 0; i < len; i++) {
+      double term = tid == 0 ? (s.Ma[i] - s.qfrc_smooth[i]) * (qacc[i] - s.qacc_smooth[i])
+                             : (s.rowflag[i] ? s.u.row.F[i] : 0.0);
+      if (tid == 0 || s.rowflag[i]) acc += term;
+    }
+    s.tmpv[tid] = acc;
+  }
+  SYNC();
   if (tid == 0) {
-    double g = 0;
-    for (int k = 0; k < nv; k++) g += (s.Ma[k] - s.qfrc_smooth[k]) * (qacc[k] - s.qacc_smooth[k]);
-    s.gauss = 0.5 * g;
-    double cost = 0;
-    for (int i = 0; i < s.nefc; i++)
-      if (s.rowflag[i]) cost += s.u.row.F[i];
-    s.cost = s.gauss + cost;
+    s.gauss = 0.5 * s.tmpv[0];
+    s.cost = s.gauss + s.tmpv[1];
   }
   SYNC();
 }
@@ -937,20 +1024,26 @@ __device__ static void w_hessian_factor(KModel m, KS& s) {
     s.H[r][c] = h;
   }
   SYNC();
-  /* Cholesky H = L L' (lower), column by column */
+  WT(10);
+  /* Cholesky H = L L' (lower), right-looking: element (i,k) receives the updates
+     -= L[i][j]*L[k][j] for j = 0,1,... in the same order as the oracle's left-looking loop */
   for (int j = 0; j < nv; j++) {
     if (tid == 0) {
       double sum = s.H[j][j];
-      for (int k = 0; k < j; k++) sum -= s.H[j][k] * s.H[j][k];
       if (sum < K_MINVAL) sum = K_MINVAL;
       s.H[j][j] = sqrt(sum);
     }
     SYNC();
     double ljj = s.H[j][j];
-    for (int i = j + 1 + tid; i < nv; i += NT) {
-      double v = s.H[i][j];
-      for (int k = 0; k < j; k++) v -= s.H[i][k] * s.H[j][k];
-      s.H[i][j] = v / ljj;
+    for (int i = j + 1 + tid; i < nv; i += NT) s.H[i][j] = s.H[i][j] / ljj;
+    SYNC();
+    const int nt = nv - j - 1; /* trailing block (j+1..nv-1), lower triangle incl. diagonal */
+    const int nel2 = nt * (nt + 1) / 2;
+    for (int e = tid; e < nel2; e += NT) {
+      int a = 0, rem = e;
+      while (rem > a) { rem -= a + 1; a++; }
+      int i = j + 1 + a, k = j + 1 + rem;
+      s.H[i][k] -= s.H[i][j] * s.H[k][j];
     }
     SYNC();
   }
@@ -1048,21 +1141,18 @@ __device__ static void w_ls_eval(KModel m, KS& s, double a) {
     s.rowflag[i] = flag;
   }
   SYNC();
-  if (tid == 0) {
-    double F = s.gauss + a * s.g1 + 0.5 * a * a * s.g2;
-    double dF = s.g1 + a * s.g2;
-    double d2F = s.g2;
+  /* lanes 0/1/2 accumulate F / dF / d2F in row order (same sequence as the oracle, run side by side) */
+  if (tid < 3) {
+    double acc = tid == 0 ? s.gauss + a * s.g1 + 0.5 * a * a * s.g2 : (tid == 1 ? s.g1 + a * s.g2 : s.g2);
+    const double* arr = tid == 0 ? s.u.row.F : (tid == 1 ? s.u.row.dF : s.u.row.d2F);
     for (int i = 0; i < nefc; i++) {
       int f = s.rowflag[i];
-      if (f) {
-        F += s.u.row.F[i];
-        dF += s.u.row.dF[i];
-        if (f == 1) d2F += s.u.row.d2F[i];
-      }
+      if (f && (tid < 2 || f == 1)) acc += arr[i];
     }
-    s.lsF = F; s.lsdF = dF; s.lsd2F = d2F;
+    s.tmpv[tid] = acc;
   }
   SYNC();
+  s.lsF = s.tmpv[0]; s.lsdF = s.tmpv[1]; s.lsd2F = s.tmpv[2];
 }
 
 template <int NT>
@@ -1089,13 +1179,11 @@ __device__ static double w_line_search(KModel m, KS& s) {
   SYNC();
   double snorm = s.sred;
   if (snorm < K_MINVAL) return 0;
-  if (tid == 0) {
-    double g1 = 0, g2 = 0;
-    for (int k = 0; k < nv; k++) {
-      g1 += s.search[k] * (s.Ma[k] - s.qfrc_smooth[k]);
-      g2 += s.search[k] * s.Mv[k];
-    }
-    s.g1 = g1; s.g2 = g2;
+  if (tid < 2) {
+    double acc = 0;
+    for (int k = 0; k < nv; k++) acc += s.search[k] * (tid == 0 ? (s.Ma[k] - s.qfrc_smooth[k]) : s.Mv[k]);
+    if (tid == 0) s.g1 = acc;
+    else s.g2 = acc;
   }
   SYNC();
   double gtol = m->tolerance * m->ls_tolerance * snorm / s.scale;
@@ -1152,18 +1240,23 @@ __device__ static void w_solve_newton(KModel m, KS& s) {
     w_eval_state<NT>(m, s, s.qacc);
   }
   w_compute_grad<NT>(m, s);
+  WT(9);
   w_hessian_factor<NT>(m, s);
+  WT(11);
   w_hessian_solve<NT>(m, s, s.xv, s.grad);
   if (tid < nv) s.search[tid] = -s.xv[tid];
   SYNC();
+  WT(12);
   for (int iter = 0; iter < m->iterations; iter++) {
     double alpha = w_line_search<NT>(m, s);
+    WT(13);
     if (alpha == 0) break;
     if (tid < nv) s.qacc[tid] += alpha * s.search[tid];
     SYNC();
     double oldcost = s.cost;
     w_eval_state<NT>(m, s, s.qacc);
     w_compute_grad<NT>(m, s);
+    WT(14);
     if (tid == 0) {
       double gn = 0;
       for (int k = 0; k < nv; k++) gn += s.grad[k] * s.grad[k];
@@ -1174,9 +1267,11 @@ __device__ static void w_solve_newton(KModel m, KS& s) {
     double gradient = s.scale * sqrt(s.sred);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
     w_hessian_factor<NT>(m, s);
+    WT(11);
     w_hessian_solve<NT>(m, s, s.xv, s.grad);
     if (tid < nv) s.search[tid] = -s.xv[tid];
     SYNC();
+    WT(12);
   }
 }
 
@@ -1187,18 +1282,29 @@ template <int NT>
 __device__ static void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
+  WT_START();
   w_kinematics<NT>(m, pl, s);
+  WT(0);
   w_com_pos<NT>(m, pl, s);
+  WT(1);
   w_crb<NT>(m, s);
-  for (int e = tid; e < nv * nv; e += NT) s.qLD[e / nv][e % nv] = s.qM[e / nv][e % nv];
+  for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
   SYNC();
-  w_factor_tree<NT>(m, pl, s.qLD, s.LDinv, s.tmpv);
+  WT(2);
+  w_factor_tree<NT>(m, pl, s.H, s.LDinv, s.tmpv);
+  WT(3);
   w_collision<NT>(m, s);
+  WT(4);
   w_make_constraint<NT>(m, pl, s);
+  WT(5);
   w_com_vel<NT>(m, pl, s);
+  WT(6);
   w_rne_passive<NT>(m, pl, s);
-  w_solve_tree<NT>(m, pl, s.qLD, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+  WT(7);
+  w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+  WT(8);
   w_solve_newton<NT>(m, s);
+  WT(15);
 }
 
 template <int NT>
@@ -1249,6 +1355,7 @@ __device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (tid < nv) s.xv[tid] = s.qacc[tid];
     SYNC();
   }
+  WT(16);
   double h = m->timestep;
   if (tid < nv) s.qvel[tid] += h * s.xv[tid];
   SYNC();
@@ -1272,6 +1379,7 @@ __device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   if (tid < nv) s.warm[tid] = s.qacc[tid];
   SYNC();
+  WT(17);
 }
 
 #endif /* UR3E_WAVE_H */

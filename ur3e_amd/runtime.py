@@ -19,7 +19,7 @@ import numpy as np
 from .model.compiler import UR3eModelC, load_json, to_ctypes
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libur3e_amd.so")
+LIB_PATH = os.environ.get("UR3E_LIB", os.path.join(_HERE, "_lib", "libur3e_amd.so"))
 ASSETS = os.path.join(_HERE, "assets")
 
 TASK_GYM_V2, TASK_TRAJ_L, TASK_MOVE_J, TASK_CTRL = 0, 1, 2, 3
