@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 1
+#define UR3E_ABI_VERSION 2
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -65,9 +65,16 @@ typedef struct ur3e_config_t {
   double joint_gains[12];/* kp[6], kd[6] (config_j.yml) */
   unsigned long long seed; /* Philox key for reset noise */
   int env_id_offset;     /* global id of local env 0 (multi-GPU shards) */
-  int envs_per_block;    /* kernel layout: 0 (default) = one 128-lane workgroup per env, working set in
-                            LDS (v2); -64 = one 64-lane wavefront per env (v2); 1..64 = one env per
-                            lane with that many envs per wavefront (v1, lane-private scratch) */
+  int envs_per_block;    /* kernel layout:
+                            0 (default) = two-tier: one 64-lane wavefront per env with a compact
+                              LDS working set (<= W_SMALL_MAXCON contacts / W_SMALL_MAXEFC rows,
+                              four envs per CU); an env that exceeds it in any substep is
+                              recomputed, same step, by the full-capacity tier;
+                            -128 = full-capacity tier only, 128-lane workgroup per env;
+                            -64 = full-capacity tier only, 64-lane wavefront per env;
+                            1..64 = one env per lane, that many envs per wavefront (v1) */
+  int tier_con_cap;      /* diagnostic (0 = off): the compact tier treats more than this many
+                            contacts as overflow, to exercise the fallback path */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;
@@ -98,6 +105,9 @@ int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const double* d_
    d_nwarn [N] bad-value auto-resets (each may be NULL) */
 int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, double* d_ep_return, int* d_nwarn,
                         void* stream);
+
+/* envs the compact tier handed to the full-capacity tier since create (synchronises) */
+int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 
 /* sizes */
 int ur3e_batch_num_envs(const ur3e_batch_t* b);

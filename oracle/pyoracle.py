@@ -37,6 +37,7 @@ class OracleConfig(ctypes.Structure):
         ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
+        ("tier_con_cap", ctypes.c_int),
     ]
 
 

@@ -32,6 +32,7 @@ typedef struct {
   unsigned long long seed;
   int env_id_offset;
   int envs_per_block;
+  int tier_con_cap;
 } ur3o_config;
 
 static void gains_from_cfg(const ur3o_config* c, ur3o_task_gains* tg, ur3o_joint_gains* jg) {

@@ -29,12 +29,13 @@ def _oracle_cfg(po, c):
     return oc
 
 
-def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1):
+def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1, tier_con_cap=0):
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model(model_name)
     cfg = rt.make_config(task=task, frame_skip=frame_skip, model=md, seed=seed, envs_per_block=epb,
+                         tier_con_cap=tier_con_cap,
                          reset_noise=(model_name == "main"),
                          reset_key=md["id_key_down"] if md["id_key_down"] >= 0 else -1)
     gb = rt.Batch(mc, cfg, n)
@@ -64,8 +65,9 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
             info = gb.get_info()
             np.testing.assert_array_equal(info["ncon"].cpu().numpy(), onc, err_msg=f"ncon step {s}")
     assert max_dq <= 1e-5
+    gb.ovf = gb.overflow_count()
     gb.close()
-    return ob
+    return gb
 
 
 def _gym_actions(rng, n, md):
@@ -74,23 +76,37 @@ def _gym_actions(rng, n, md):
     return rng.uniform(lo, hi, size=(n, 4))
 
 
-# kernel layouts: 0 = workgroup-per-env (128 lanes, default), -64 = one wavefront per env,
-# 16 = one env per lane (16 envs per wavefront, v1)
-@pytest.mark.parametrize("epb", [0, -64, 16])
+# kernel layouts: 0 = two-tier (compact 64-lane tier + full-capacity fallback, default),
+# -128 / -64 = full-capacity tier only with 128 / 64 lanes per env, 16 = one env per lane (v1)
+@pytest.mark.parametrize("epb", [0, -128, -64, 16])
 def test_gym_v2_random_actions_short(epb):
     _run_pair("main", 0, 64, 60, _gym_actions, epb=epb)
 
 
-def test_gym_v2_grasp_region():
+def _grasp_actions(rng, n, md):
     # actions concentrated around the mug with the gripper closing: exercises pad-box contacts
-    def act(rng, n, md):
-        a = np.zeros((n, 4))
-        a[:, 0] = 0.29799994 + rng.normal(size=n) * 0.01
-        a[:, 1] = 0.13349916 + rng.normal(size=n) * 0.01
-        a[:, 2] = rng.uniform(0.02, 0.12, size=n)
-        a[:, 3] = rng.uniform(0.5, 1.0, size=n)
-        return a
-    _run_pair("main", 0, 64, 150, act, seed=3)
+    a = np.zeros((n, 4))
+    a[:, 0] = 0.29799994 + rng.normal(size=n) * 0.01
+    a[:, 1] = 0.13349916 + rng.normal(size=n) * 0.01
+    a[:, 2] = rng.uniform(0.02, 0.12, size=n)
+    a[:, 3] = rng.uniform(0.5, 1.0, size=n)
+    return a
+
+
+def test_gym_v2_grasp_region():
+    _run_pair("main", 0, 64, 150, _grasp_actions, seed=3)
+
+
+@pytest.mark.parametrize("cap", [2, 3])
+def test_two_tier_fallback(cap):
+    """Compact-tier overflow mid-step (the diagnostic cap makes envs with more than `cap` contacts
+    overflow in either substep or in an auto-reset) hands the env to the full-capacity tier, which
+    recomputes the step from the untouched state: results stay bit-exact, the fallback is taken,
+    and (cap 3) some env-steps still complete in the compact tier."""
+    gb = _run_pair("main", 0, 64, 80, _grasp_actions, seed=11, tier_con_cap=cap)
+    assert gb.ovf > 0
+    if cap == 3:
+        assert gb.ovf < 64 * 80
 
 
 def test_move_j_2f85():

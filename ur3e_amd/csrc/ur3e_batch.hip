@@ -303,6 +303,7 @@ struct KConfig {
   unsigned long long seed;
   int env_id_offset;
   int epb;
+  int tier_con_cap;
   KGains gains;
 };
 
@@ -468,8 +469,8 @@ __global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __rest
 /* workgroup-per-env kernels (v2, default): see ur3e_wave.h            */
 /* ================================================================== */
 /* carry from the LDS working set: tcp pose, arm Jacobian (6x6), qfrc_bias[0:6] */
-template <int NT>
-__device__ static void w_make_carry(KModel m, const KPlan* __restrict__ pl, const KS& s, double* carry) {
+template <int NT, class KS>
+WD void w_make_carry(KModel m, const KPlan* __restrict__ pl, const KS& s, double* carry) {
   const int tid = threadIdx.x;
   int st = m->id_site_tcp;
   if (st < 0) {
@@ -502,6 +503,7 @@ __device__ static void w_make_carry(KModel m, const KPlan* __restrict__ pl, cons
   }
 }
 
+template <class KS>
 KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
   int b = m->site_bodyid[site];
   const double* cv = s.cvel[b];
@@ -514,6 +516,7 @@ KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
 }
 
 /* UR3eEnv2._get_obs (ur3e_env2.py:111-123), lane 0 */
+template <class KS>
 KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
   int st = m->id_site_tcp, sh = m->id_site_handle, gb = m->id_body_ghost;
   const double* tcp = s.site_xpos[st];
@@ -548,6 +551,7 @@ KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
   obs[23] = (double)robust;
 }
 
+template <class KS>
 KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
   double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
   if (1.0 < sqrt(dx * dx + dy * dy + dz * dz)) return 1;
@@ -564,42 +568,67 @@ KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
   return 0;
 }
 
+/* per-env step results staged in LDS; nothing reaches global memory before w_commit, so a
+   compact-tier env that overflows (s.ovf) can be recomputed from its untouched state */
 struct WOut {
   double obs[24];
+  double tobs[24];
   double carry[NCARRY];
   double a[8];
-  double r;
-  int term, trunc, t;
+  double r, ep_return;
+  int term, trunc, t, ep_len, did_reset;
+  unsigned int episode;
 };
 
-template <int NT>
-__device__ static void w_load(KModel m, const KState& st, int e, KS& s) {
+template <int NT, class KS>
+WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut& o) {
   const int tid = threadIdx.x;
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = st.qpos[SQ(st, k, e)];
   for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = st.qvel[SV(st, k, e)]; s.warm[k] = st.warm[SV(st, k, e)]; }
-  if (tid == 0) s.nwarn = st.nwarn[e];
+  if (tid == 0) {
+    s.nwarn = st.nwarn[e];
+    s.ovf = 0;
+    s.cap_con = (KS::BAIL && c.tier_con_cap > 0 && c.tier_con_cap < KS::MAXCON) ? c.tier_con_cap : KS::MAXCON;
+    o.t = st.t[e]; o.ep_len = st.ep_len[e]; o.ep_return = st.ep_return[e]; o.episode = st.episode[e];
+    o.did_reset = 0; o.term = 0; o.trunc = 0; o.r = 0;
+  }
 }
 
-template <int NT>
-__device__ static void w_store(KModel m, const KState& st, int e, const KS& s, const double* carry) {
+/* the single write-back point of every v2 kernel */
+template <int NT, class KS>
+WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& s, const WOut& o, double* obs_out,
+                 double* rew_out, unsigned char* term_out, unsigned char* trunc_out, double* tobs_out, int stepped) {
   const int tid = threadIdx.x;
   for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
-  for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = carry[k];
-  if (tid == 0) { st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn; }
+  for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
+  if (tid == 0) {
+    st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
+    st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
+    if (stepped && c.task == UR3E_TASK_GYM_V2) {
+      if (rew_out) rew_out[e] = o.r;
+      if (term_out) term_out[e] = (unsigned char)o.term;
+      if (trunc_out) trunc_out[e] = (unsigned char)o.trunc;
+    }
+  }
+  if (c.task == UR3E_TASK_GYM_V2) {
+    if (stepped && o.did_reset && tobs_out)
+      for (int k = tid; k < 24; k += NT) tobs_out[(size_t)e * 24 + k] = o.tobs[k];
+    if (obs_out)
+      for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
+  }
 }
 
 /* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
-template <int NT>
-__device__ static void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
-                                   KS& s, WOut& o) {
+template <int NT, class KS>
+WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, int e, KS& s, WOut& o) {
   const int tid = threadIdx.x;
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = c.reset_key >= 0 ? m->key_qpos[c.reset_key][k] : m->qpos0[k];
   for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = c.reset_key >= 0 ? m->key_qvel[c.reset_key][k] : 0.0; s.warm[k] = 0; }
   for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
   SYNC();
   if (tid == 0) {
-    unsigned int ep = st.episode[e];
+    unsigned int ep = o.episode;
     if (c.reset_noise && m->id_body_fish >= 0) {
       unsigned int gid = (unsigned int)(c.env_id_offset + e);
       double u0 = k_uniform01(c.seed, gid, ep, 0);
@@ -608,45 +637,25 @@ __device__ static void w_reset_env(KModel m, const KPlan* __restrict__ pl, const
       s.qpos[15] += -0.25 + (0.2 - -0.25) * u1;
     }
     s.nwarn = 0;
-    st.t[e] = 0;
-    st.ep_len[e] = 0;
-    st.ep_return[e] = 0;
-    st.episode[e] = ep + 1;
+    o.t = 0;
+    o.ep_len = 0;
+    o.ep_return = 0;
+    o.episode = ep + 1;
   }
   SYNC();
   w_forward<NT>(m, pl, s);
+  if (KS::BAIL && s.ovf) return;
   if (tid == 0 && c.task == UR3E_TASK_GYM_V2) w_obs_v2(m, s, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
-                                                   KConfig c, KState st, const unsigned char* __restrict__ mask,
-                                                   double* __restrict__ obs_out) {
-  __shared__ KS s;
-  __shared__ WOut o;
-  const int e = blockIdx.x, tid = threadIdx.x;
-  if (e >= st.n) return;
-  if (mask && !mask[e]) return;
-  w_reset_env<NT>(m, pl, c, st, e, s, o);
-  w_store<NT>(m, st, e, s, o.carry);
-  if (obs_out && c.task == UR3E_TASK_GYM_V2)
-    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
-}
-
-template <int NT>
-__global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
-                                                  KConfig c, KState st, const double* __restrict__ actions, int adim,
-                                                  double* __restrict__ obs_out, double* __restrict__ rew_out,
-                                                  unsigned char* __restrict__ term_out,
-                                                  unsigned char* __restrict__ trunc_out,
-                                                  double* __restrict__ tobs_out) {
-  __shared__ KS s;
-  __shared__ WOut o;
-  const int e = blockIdx.x, tid = threadIdx.x;
-  if (e >= st.n) return;
-  w_load<NT>(m, st, e, s);
+/* one env-step of env e into LDS (s, o); false: the compact tier overflowed */
+template <int NT, class KS>
+WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
+                        const double* __restrict__ actions, int adim, KS& s, WOut& o) {
+  const int tid = threadIdx.x;
+  w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
   for (int k = tid; k < NCARRY; k += NT) o.carry[k] = st.carry[SC(st, k, e)];
   SYNC();
@@ -686,17 +695,20 @@ __global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict_
   }
   SYNC();
   int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
-  for (int sstep = 0; sstep < fs; sstep++) w_step<NT>(m, pl, s);
+  for (int sstep = 0; sstep < fs; sstep++) {
+    w_step<NT>(m, pl, s);
+    if (KS::BAIL && s.ovf) return false;
+  }
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
   if (c.task != UR3E_TASK_GYM_V2) {
-    if (tid == 0) { st.t[e] += 1; st.ep_len[e] += 1; }
-    w_store<NT>(m, st, e, s, o.carry);
-    return;
+    if (tid == 0) { o.t += 1; o.ep_len += 1; }
+    SYNC();
+    return true;
   }
   if (tid == 0) {
-    int t = st.t[e] + 1;
-    st.t[e] = t;
+    int t = o.t + 1;
+    o.t = t;
     w_obs_v2(m, s, o.obs);
     double r = k_reward_v2(o.obs, o.a);
     int term = w_termination_v2(m, s, o.obs);
@@ -706,24 +718,81 @@ __global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict_
       term = 1;
       r += 50.0;
     }
-    st.ep_return[e] += r;
-    st.ep_len[e] += 1;
-    if (rew_out) rew_out[e] = r;
-    if (term_out) term_out[e] = (unsigned char)term;
-    if (trunc_out) trunc_out[e] = (unsigned char)trunc;
+    o.ep_return += r;
+    o.ep_len += 1;
+    o.r = r;
     o.term = term;
     o.trunc = trunc;
   }
   SYNC();
   if ((o.term || o.trunc) && c.auto_reset) {
-    if (tobs_out)
-      for (int k = tid; k < 24; k += NT) tobs_out[(size_t)e * 24 + k] = o.obs[k];
+    for (int k = tid; k < 24; k += NT) o.tobs[k] = o.obs[k];
+    if (tid == 0) o.did_reset = 1;
     SYNC();
-    w_reset_env<NT>(m, pl, c, st, e, s, o);
+    w_reset_env<NT>(m, pl, c, e, s, o);
+    if (KS::BAIL && s.ovf) return false;
   }
-  w_store<NT>(m, st, e, s, o.carry);
-  if (obs_out)
-    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
+  return true;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+                                                   KConfig c, KState st, const unsigned char* __restrict__ mask,
+                                                   double* __restrict__ obs_out) {
+  __shared__ KSL s;
+  __shared__ WOut o;
+  const int e = blockIdx.x;
+  if (e >= st.n) return;
+  if (mask && !mask[e]) return;
+  w_load<NT>(m, c, st, e, s, o);
+  SYNC();
+  w_reset_env<NT>(m, pl, c, e, s, o);
+  w_commit<NT>(m, c, st, e, s, o, obs_out, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+/* one env per workgroup; a compact-tier (KS::BAIL) env that overflows is queued on ovf_list
+   for w_env_step_list and writes nothing */
+template <int NT, class KS>
+__global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+                                                  KConfig c, KState st, const double* __restrict__ actions, int adim,
+                                                  double* __restrict__ obs_out, double* __restrict__ rew_out,
+                                                  unsigned char* __restrict__ term_out,
+                                                  unsigned char* __restrict__ trunc_out,
+                                                  double* __restrict__ tobs_out, int* __restrict__ ovf_list,
+                                                  int* __restrict__ ovf_count) {
+  __shared__ KS s;
+  __shared__ WOut o;
+  const int e = blockIdx.x;
+  if (e >= st.n) return;
+  if (!w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o)) {
+    if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = e;
+    return;
+  }
+  w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+}
+
+/* full-capacity tier over the envs the compact tier queued (grid-stride over the list) */
+template <int NT>
+__global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __restrict__ m,
+                                                       const KPlan* __restrict__ pl, KConfig c, KState st,
+                                                       const double* __restrict__ actions, int adim,
+                                                       double* __restrict__ obs_out, double* __restrict__ rew_out,
+                                                       unsigned char* __restrict__ term_out,
+                                                       unsigned char* __restrict__ trunc_out,
+                                                       double* __restrict__ tobs_out,
+                                                       const int* __restrict__ ovf_list,
+                                                       const int* __restrict__ ovf_count,
+                                                       unsigned long long* __restrict__ ovf_total) {
+  __shared__ KSL s;
+  __shared__ WOut o;
+  const int cnt = *ovf_count;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const int e = ovf_list[i];
+    w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
+    w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+    SYNC();
+  }
 }
 
 template <int NT>
@@ -732,22 +801,23 @@ __global__ __launch_bounds__(NT) void w_env_set_state(const ur3e_model_t* __rest
                                                        const double* __restrict__ qpos,
                                                        const double* __restrict__ qvel,
                                                        const double* __restrict__ warm) {
-  __shared__ KS s;
+  __shared__ KSL s;
   __shared__ WOut o;
   const int e = blockIdx.x, tid = threadIdx.x;
   if (e >= st.n) return;
+  w_load<NT>(m, c, st, e, s, o);
+  SYNC();
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = qpos[(size_t)e * m->nq + k];
   for (int k = tid; k < m->nv; k += NT) {
     s.qvel[k] = qvel[(size_t)e * m->nv + k];
-    s.warm[k] = warm ? warm[(size_t)e * m->nv + k] : st.warm[SV(st, k, e)];
+    if (warm) s.warm[k] = warm[(size_t)e * m->nv + k];
   }
   for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
-  if (tid == 0) s.nwarn = st.nwarn[e];
   SYNC();
   w_forward<NT>(m, pl, s);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
-  w_store<NT>(m, st, e, s, o.carry);
+  w_commit<NT>(m, c, st, e, s, o, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
 }
 
 /* create(): qpos0 / zero velocities, episode 0; envs are valid after ur3e_batch_reset */
@@ -788,6 +858,10 @@ struct ur3e_batch {
   int device;
   int n;
   int wave_nt; /* 0: lane-per-env kernels (v1); 64/128: workgroup-per-env kernels (v2) */
+  int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
+  int* d_ovf_list;
+  int* d_ovf_count;
+  unsigned long long* d_ovf_total;
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
@@ -864,6 +938,10 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   if ((cfg->task == UR3E_TASK_GYM_V2 || cfg->task == UR3E_TASK_TRAJ_L) && model->id_site_tcp < 0)
     return fail(UR3E_EMODEL, "task-space control needs the tcp site");
   if (cfg->reset_key >= model->nkey) return fail(UR3E_EINVAL, "reset_key out of range");
+  if (cfg->envs_per_block > 64) return fail(UR3E_EINVAL, "envs_per_block > 64");
+  /* 0: two-tier (default); -64: full-capacity tier, 64 lanes; other negative: full-capacity tier,
+     128 lanes; 1..64: v1 lane-per-env */
+  int tiered = cfg->envs_per_block == 0;
   int wave_nt = cfg->envs_per_block == 0 ? 128 : (cfg->envs_per_block == -64 ? 64 : (cfg->envs_per_block < 0 ? 128 : 0));
   if (wave_nt && model->ncpair > W_MAXCAND) return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
   HIPCHK(hipSetDevice(device));
@@ -871,6 +949,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->device = device;
   b->n = n_envs;
   b->wave_nt = wave_nt;
+  b->tiered = tiered;
   b->host_model = *model;
   b->timed = 0;
   KConfig& c = b->cfg;
@@ -883,6 +962,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.seed = cfg->seed;
   c.env_id_offset = cfg->env_id_offset;
   c.epb = cfg->envs_per_block > 0 && cfg->envs_per_block <= 64 ? cfg->envs_per_block : 16;
+  c.tier_con_cap = cfg->tier_con_cap;
   KPlan plan;
   build_plan(model, &plan);
   for (int k = 0; k < 12; k++) { c.gains.task[k] = cfg->task_gains[k]; c.gains.joint[k] = cfg->joint_gains[k]; }
@@ -910,6 +990,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMalloc(&s.nwarn, sizeof(int) * nd));
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&b->d_ovf_count, sizeof(int)));
+  HIPCHK(hipMalloc(&b->d_ovf_total, sizeof(unsigned long long)));
+  HIPCHK(hipMemset(b->d_ovf_count, 0, sizeof(int)));
+  HIPCHK(hipMemset(b->d_ovf_total, 0, sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
   /* qpos0 / zero state; like a gymnasium Env, call ur3e_batch_reset before the first step */
@@ -924,7 +1009,8 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
   void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
-                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn};
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->d_ovf_list, b->d_ovf_count,
+                  b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   (void)hipEventDestroy(b->ev0);
   (void)hipEventDestroy(b->ev1);
@@ -958,12 +1044,23 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   HIPCHK(hipSetDevice(b->device));
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipEventRecord(b->ev0, st));
-  if (b->wave_nt == 128)
-    hipLaunchKernelGGL(w_env_step<128>, dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st, d_actions,
-                       adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+  if (b->tiered) {
+    HIPCHK(hipMemsetAsync(b->d_ovf_count, 0, sizeof(int), st));
+    hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_count);
+    int grid = b->n < 512 ? b->n : 512;
+    hipLaunchKernelGGL(w_env_step_list<128>, dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_count, b->d_ovf_total);
+  } else if (b->wave_nt == 128)
+    hipLaunchKernelGGL((w_env_step<128, KSL>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_count);
   else if (b->wave_nt == 64)
-    hipLaunchKernelGGL(w_env_step<64>, dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st, d_actions,
-                       adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
+    hipLaunchKernelGGL((w_env_step<64, KSL>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_count);
   else
     hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
                        d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
@@ -1025,6 +1122,14 @@ extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long
   (void)cycles; (void)calls; (void)reset;
   return fail(UR3E_EINVAL, "library built without -DUR3E_STAGE_TIMING");
 #endif
+}
+
+extern "C" int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total) {
+  if (!b || !total) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(total, b->d_ovf_total, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return UR3E_OK;
 }
 
 extern "C" int ur3e_batch_num_envs(const ur3e_batch_t* b) { return b ? b->n : 0; }

@@ -48,7 +48,14 @@ struct KPlan {
 #define G_LIMIT 3
 #define G_CONTACT 4
 
-struct KS {
+template <int MC, int ME>
+struct KSX {
+  static constexpr int MAXCON = MC; /* contacts this tier holds */
+  static constexpr int MAXEFC = ME; /* constraint rows this tier holds */
+  static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
+  /* a tier smaller than the oracle's capacity never clamps: it flags the env
+     (ovf) and the env-step is recomputed by the full-capacity tier */
+  static constexpr bool BAIL = (MC < K_MAXCON) || (ME < K_MAXEFC);
   /* state */
   double qpos[K_NQ], qvel[K_NV], warm[K_NV], ctrl[K_NU];
   /* position stage */
@@ -73,25 +80,38 @@ struct KS {
       double b6[K_NB][6];
     } body;
     struct {
-      double F[K_MAXEFC], dF[K_MAXEFC], d2F[K_MAXEFC];
+      double F[ME], dF[ME], d2F[ME];
     } row;
   } u;
   /* contacts */
-  double con_pos[K_MAXCON][3], con_frame[K_MAXCON][9], con_dist[K_MAXCON], con_mu[K_MAXCON];
-  double con_Hc[K_MAXCON][9];
-  int con_geom1[K_MAXCON], con_geom2[K_MAXCON], con_cpair[K_MAXCON], con_efc[K_MAXCON];
+  double con_pos[MC][3], con_frame[MC][9], con_dist[MC], con_mu[MC];
+  double con_Hc[MC][9];
+  int con_geom1[MC], con_geom2[MC], con_cpair[MC], con_efc[MC];
   int cand_count[W_MAXCAND], cand_off[W_MAXCAND];
   /* constraint rows */
-  double efc_J[K_MAXEFC][K_NV];
-  double efc_R[K_MAXEFC], efc_D[K_MAXEFC], efc_aref[K_MAXEFC], efc_floss[K_MAXEFC];
-  double efc_force[K_MAXEFC], jar[K_MAXEFC], Jv[K_MAXEFC];
-  int efc_type[K_MAXEFC], efc_id[K_MAXEFC], efc_state[K_MAXEFC], rowflag[K_MAXEFC], efc_grp[K_MAXEFC];
-  int grp_type[W_MAXGRP], grp_id[W_MAXGRP], grp_row[W_MAXGRP];
+  double efc_J[ME][K_NV];
+  double efc_R[ME], efc_D[ME], efc_aref[ME], efc_floss[ME];
+  double efc_force[ME], jar[ME], Jv[ME];
+  int efc_type[ME], efc_id[ME], efc_state[ME], rowflag[ME], efc_grp[ME];
+  int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
   /* scalars */
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
-  int ncon, nefc, ngrp, nwarn, flag;
+  int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
   unsigned long long tlast;
 };
+/* full-capacity tier: the oracle's limits (UR3E_MAXCON contacts, UR3E_MAXEFC rows) */
+typedef KSX<K_MAXCON, K_MAXEFC> KSL;
+/* compact tier: sized for the contact/row counts main.xml actually reaches
+   (<= 8 contacts, <= 38 rows over long random and grasp rollouts; 13 fixed rows +
+   3 per contact), small enough
+   for four envs (four wavefronts) per CU */
+#ifndef W_SMALL_MAXCON
+#define W_SMALL_MAXCON 10
+#endif
+#ifndef W_SMALL_MAXEFC
+#define W_SMALL_MAXEFC 44
+#endif
+typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
    wave's LDS instructions issue and complete in program order, so cross-lane LDS hand-offs only
@@ -107,6 +127,7 @@ __device__ __forceinline__ void wsync() {
   }
 }
 #define SYNC() wsync<NT>()
+#define WD __device__ static __forceinline__
 
 /* diagnostic build only (-DUR3E_STAGE_TIMING): per-stage shader-clock cycles, lane 0 of every env */
 #ifdef UR3E_STAGE_TIMING
@@ -137,8 +158,8 @@ __device__ unsigned long long ur3e_stage_calls[32];
 /* ================================================================== */
 /* kinematics (level-parallel over bodies)                             */
 /* ================================================================== */
-template <int NT>
-__device__ static void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   if (tid == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
@@ -208,8 +229,8 @@ __device__ static void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& 
 /* ================================================================== */
 /* com_pos: subtree com, cinert, cdof                                  */
 /* ================================================================== */
-template <int NT>
-__device__ static void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nb = m->nbody;
   double xipos[3] = {0, 0, 0}, ximat[9];
@@ -311,8 +332,8 @@ __device__ static void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) 
 /* ================================================================== */
 /* CRB mass matrix + tree LDL'                                         */
 /* ================================================================== */
-template <int NT>
-__device__ static void w_crb(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_crb(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nb = m->nbody, nv = m->nv;
   for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
@@ -344,7 +365,7 @@ __device__ static void w_crb(KModel m, KS& s) {
 
 /* A (K_NV x K_NV in LDS) -> reverse tree LDL' in place, diaginv */
 template <int NT>
-__device__ static void w_factor_tree(KModel m, const KPlan* __restrict__ pl, double (*A)[K_NV], double* diaginv,
+WD void w_factor_tree(KModel m, const KPlan* __restrict__ pl, double (*A)[K_NV], double* diaginv,
                                      double* tmp) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
@@ -377,7 +398,7 @@ __device__ static void w_factor_tree(KModel m, const KPlan* __restrict__ pl, dou
 
 /* x = A^-1 b with the tree factor; x, b in LDS (may alias) */
 template <int NT>
-__device__ static void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K_NV],
+WD void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K_NV],
                                     const double* diaginv, double* x, const double* b) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
@@ -399,7 +420,8 @@ __device__ static void w_solve_tree(KModel m, const KPlan* __restrict__ pl, cons
 /* ================================================================== */
 /* collision: per-candidate lanes, prefix offsets, deterministic order */
 /* ================================================================== */
-__device__ static int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
+template <class KS>
+WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
   int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   double margin = m->cpair_margin[p];
   double rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
@@ -420,8 +442,8 @@ __device__ static int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
   return 0;
 }
 
-template <int NT>
-__device__ static void w_collision(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_collision(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int np = m->ncpair;
   KRaw raw[8];
@@ -433,15 +455,17 @@ __device__ static void w_collision(KModel m, KS& s) {
       s.cand_off[p] = off;
       off += s.cand_count[p];
     }
-    s.ncon = off < K_MAXCON ? off : K_MAXCON;
+    s.ncon = off < KS::MAXCON ? off : KS::MAXCON;
+    if (KS::BAIL && off > s.cap_con) s.ovf = 1;
   }
   SYNC();
+  if (KS::BAIL && s.ovf) return;
   for (int p = tid; p < np; p += NT) {
     int cnt = s.cand_count[p];
     int off = s.cand_off[p];
-    if (cnt == 0 || off >= K_MAXCON) continue;
+    if (cnt == 0 || off >= KS::MAXCON) continue;
     int n = w_narrow(m, s, p, raw);
-    for (int k = 0; k < n && off + k < K_MAXCON; k++) {
+    for (int k = 0; k < n && off + k < KS::MAXCON; k++) {
       int c = off + k;
       s.con_pos[c][0] = raw[k].pos[0]; s.con_pos[c][1] = raw[k].pos[1]; s.con_pos[c][2] = raw[k].pos[2];
       k_make_frame(s.con_frame[c], raw[k].n);
@@ -460,6 +484,7 @@ __device__ static void w_collision(KModel m, KS& s) {
 /* constraint rows                                                     */
 /* ================================================================== */
 /* translational point-Jacobian column v of `body` at p (zero outside the chain) */
+template <class KS>
 KD void w_jacp_col(KModel m, const KPlan* __restrict__ pl, const KS& s, int body, const double off[3], int v,
                    double out[3]) {
   if ((pl->body_dof_mask[body] >> v) & 1u) {
@@ -474,6 +499,7 @@ KD void w_jacp_col(KModel m, const KPlan* __restrict__ pl, const KS& s, int body
   }
 }
 
+template <class KS>
 KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double* simp, double pos, double margin,
                         double diag, int friction_row) {
   const int nv = m->nv;
@@ -502,8 +528,8 @@ KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double
   s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
 }
 
-template <int NT>
-__device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   /* lane 0 lays out the row groups in oracle order; a group that does not fit stops the layout */
@@ -511,12 +537,12 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
     int nrow = 0, ng = 0, stop = 0;
     for (int e = 0; e < m->neq && !stop; e++) {
       int need = m->eq_type[e] == UR3E_EQ_CONNECT ? 3 : 1;
-      if (nrow + need > K_MAXEFC) { stop = 1; break; }
+      if (nrow + need > KS::MAXEFC) { stop = 1; break; }
       s.grp_type[ng] = m->eq_type[e] == UR3E_EQ_CONNECT ? G_CONNECT : G_JOINTEQ;
       s.grp_id[ng] = e; s.grp_row[ng] = nrow; ng++; nrow += need;
     }
     for (int k = 0; k < pl->nfloss && !stop; k++) {
-      if (nrow + 1 > K_MAXEFC) { stop = 1; break; }
+      if (nrow + 1 > KS::MAXEFC) { stop = 1; break; }
       s.grp_type[ng] = G_FLOSS; s.grp_id[ng] = pl->floss_dof[k]; s.grp_row[ng] = nrow; ng++; nrow++;
     }
     for (int j = 0; j < m->njnt && !stop; j++) {
@@ -526,20 +552,22 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
       for (int side = -1; side <= 1; side += 2) {
         double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
         if (dist < m->jnt_margin[j]) {
-          if (nrow + 1 > K_MAXEFC) { stop = 1; break; }
+          if (nrow + 1 > KS::MAXEFC) { stop = 1; break; }
           s.grp_type[ng] = G_LIMIT; s.grp_id[ng] = 2 * j + (side + 1) / 2; s.grp_row[ng] = nrow; ng++; nrow++;
         }
       }
     }
     for (int c = 0; c < s.ncon && !stop; c++) {
       if (m->cpair_condim[s.con_cpair[c]] != 3) continue;
-      if (nrow + 3 > K_MAXEFC) { stop = 1; break; }
+      if (nrow + 3 > KS::MAXEFC) { stop = 1; break; }
       s.grp_type[ng] = G_CONTACT; s.grp_id[ng] = c; s.grp_row[ng] = nrow; ng++; nrow += 3;
     }
     s.ngrp = ng;
     s.nefc = nrow;
+    if (KS::BAIL && stop) s.ovf = 1;
   }
   SYNC();
+  if (KS::BAIL && s.ovf) return;
   /* phase A: Jacobian entries, one lane per (group, dof) */
   const int nitem = s.ngrp * nv;
   for (int it = tid; it < nitem; it += NT) {
@@ -677,8 +705,8 @@ __device__ static void w_make_constraint(KModel m, const KPlan* __restrict__ pl,
 /* ================================================================== */
 /* velocity stage                                                      */
 /* ================================================================== */
-template <int NT>
-__device__ static void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nb = m->nbody;
   if (tid < 6) s.cvel[0][tid] = 0;
@@ -716,8 +744,8 @@ __device__ static void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) 
   }
 }
 
-template <int NT>
-__device__ static void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nb = m->nbody, nv = m->nv;
   double (*cacc)[10] = s.u.body.b10;
@@ -825,8 +853,8 @@ __device__ static void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS&
 /* Newton solver                                                       */
 /* ================================================================== */
 /* per-row force/state and cost contribution (rowflag: adds to the cost) */
-template <int NT>
-__device__ static void w_constraint_update(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_constraint_update(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nefc = s.nefc;
   for (int i = tid; i < nefc; i += NT) {
@@ -905,8 +933,8 @@ __device__ static void w_constraint_update(KModel m, KS& s) {
   SYNC();
 }
 
-template <int NT>
-__device__ static void w_eval_state(KModel m, KS& s, const double* qacc) {
+template <int NT, class KS>
+WD void w_eval_state(KModel m, KS& s, const double* qacc) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   for (int i = tid; i < nv + s.nefc; i += NT) {
@@ -942,8 +970,8 @@ __device__ static void w_eval_state(KModel m, KS& s, const double* qacc) {
   SYNC();
 }
 
-template <int NT>
-__device__ static void w_compute_grad(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_compute_grad(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   if (tid < nv) {
@@ -956,8 +984,8 @@ __device__ static void w_compute_grad(KModel m, KS& s) {
   SYNC();
 }
 
-template <int NT>
-__device__ static void w_hessian_factor(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_hessian_factor(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   /* cone Hessians (middle zone), one lane per contact */
@@ -1050,8 +1078,8 @@ __device__ static void w_hessian_factor(KModel m, KS& s) {
 }
 
 /* x = H^-1 b by column sweeps (oracle order: forward k ascending, back k descending) */
-template <int NT>
-__device__ static void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
+template <int NT, class KS>
+WD void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   if (tid < nv) s.tmpv[tid] = b[tid];
@@ -1073,8 +1101,8 @@ __device__ static void w_hessian_solve(KModel m, KS& s, double* x, const double*
 }
 
 /* line-search 1-D evaluation at step a: per-row contributions + ordered sums on lane 0 */
-template <int NT>
-__device__ static void w_ls_eval(KModel m, KS& s, double a) {
+template <int NT, class KS>
+WD void w_ls_eval(KModel m, KS& s, double a) {
   const int tid = threadIdx.x;
   const int nefc = s.nefc;
   for (int i = tid; i < nefc; i += NT) {
@@ -1155,8 +1183,8 @@ __device__ static void w_ls_eval(KModel m, KS& s, double a) {
   s.lsF = s.tmpv[0]; s.lsdF = s.tmpv[1]; s.lsd2F = s.tmpv[2];
 }
 
-template <int NT>
-__device__ static double w_line_search(KModel m, KS& s) {
+template <int NT, class KS>
+WD double w_line_search(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   if (tid == 0) {
@@ -1217,8 +1245,8 @@ __device__ static double w_line_search(KModel m, KS& s) {
   return bestA;
 }
 
-template <int NT>
-__device__ static void w_solve_newton(KModel m, KS& s) {
+template <int NT, class KS>
+WD void w_solve_newton(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   if (s.nefc == 0) {
@@ -1278,8 +1306,8 @@ __device__ static void w_solve_newton(KModel m, KS& s) {
 /* ================================================================== */
 /* forward / step                                                      */
 /* ================================================================== */
-template <int NT>
-__device__ static void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nv = m->nv;
   WT_START();
@@ -1295,8 +1323,10 @@ __device__ static void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) 
   WT(3);
   w_collision<NT>(m, s);
   WT(4);
+  if (KS::BAIL && s.ovf) return;
   w_make_constraint<NT>(m, pl, s);
   WT(5);
+  if (KS::BAIL && s.ovf) return;
   w_com_vel<NT>(m, pl, s);
   WT(6);
   w_rne_passive<NT>(m, pl, s);
@@ -1307,8 +1337,8 @@ __device__ static void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) 
   WT(15);
 }
 
-template <int NT>
-__device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
+template <int NT, class KS>
+WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nq = m->nq, nv = m->nv;
   if (tid == 0) {
@@ -1325,6 +1355,7 @@ __device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     SYNC();
   }
   w_forward<NT>(m, pl, s);
+  if (KS::BAIL && s.ovf) return;
   if (tid == 0) {
     int bad = 0;
     for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qacc[k]);
@@ -1337,6 +1368,7 @@ __device__ static void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (tid == 0) s.nwarn++;
     SYNC();
     w_forward<NT>(m, pl, s);
+    if (KS::BAIL && s.ovf) return;
   }
   /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
   int damped = 0;

@@ -39,6 +39,7 @@ class ConfigC(ctypes.Structure):
         ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
+        ("tier_con_cap", ctypes.c_int),
     ]
 
 
@@ -60,6 +61,7 @@ def load_library():
     L.ur3e_batch_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.ur3e_batch_get_info.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ur3e_batch_last_step_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu"):
         getattr(L, f).argtypes = [vp]
     _lib = L
@@ -80,7 +82,7 @@ def load_model(name: str = "main"):
 
 def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
                 reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
-                task_gains=None, joint_gains=None) -> ConfigC:
+                task_gains=None, joint_gains=None, tier_con_cap=0) -> ConfigC:
     c = ConfigC()
     c.task = task
     c.frame_skip = frame_skip
@@ -100,6 +102,7 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.seed = seed
     c.env_id_offset = env_id_offset
     c.envs_per_block = envs_per_block
+    c.tier_con_cap = tier_con_cap
     return c
 
 
@@ -184,6 +187,12 @@ class Batch:
         nw = t.empty(self.n, dtype=t.int32, device=self.device)
         _check(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
         return dict(ncon=nc, ep_len=el, ep_return=er, nwarn=nw)
+
+    def overflow_count(self) -> int:
+        """Env-steps the compact tier handed to the full-capacity tier since create."""
+        v = ctypes.c_ulonglong()
+        _check(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
+        return int(v.value)
 
     def last_step_ms(self) -> float:
         ms = ctypes.c_float()
