@@ -102,11 +102,9 @@ def test_two_tier_fallback(cap):
     """Compact-tier overflow mid-step (the diagnostic cap makes envs with more than `cap` contacts
     overflow in either substep or in an auto-reset) hands the env to the full-capacity tier, which
     recomputes the step from the untouched state: results stay bit-exact, the fallback is taken,
-    and (cap 3) some env-steps still complete in the compact tier."""
+    including mid-step bails after a substep already ran."""
     gb = _run_pair("main", 0, 64, 80, _grasp_actions, seed=11, tier_con_cap=cap)
     assert gb.ovf > 0
-    if cap == 3:
-        assert gb.ovf < 64 * 80
 
 
 def test_move_j_2f85():

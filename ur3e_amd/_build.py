@@ -4,7 +4,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "ur3e_batch.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "ur3e_engine.h"), os.path.join(HERE, "csrc", "ur3e_wave.h"),
+DEPS = [SRC, os.path.join(HERE, "csrc", "ur3e_engine.h"), os.path.join(HERE, "csrc", "ur3e_wave.h"), os.path.join(HERE, "csrc", "ur3e_wave_r.h"),
         os.path.join(HERE, "csrc", "detmath.h"),
         os.path.join(HERE, "..", "include", "ur3e_model.h"), os.path.join(HERE, "..", "include", "ur3e_batch.h")]
 LIB = os.path.join(HERE, "_lib", "libur3e_amd.so")

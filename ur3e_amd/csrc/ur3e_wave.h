@@ -1303,6 +1303,8 @@ WD void w_solve_newton(KModel m, KS& s) {
   }
 }
 
+#include "ur3e_wave_r.h"
+
 /* ================================================================== */
 /* forward / step                                                      */
 /* ================================================================== */
@@ -1333,7 +1335,10 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   WT(7);
   w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
   WT(8);
-  w_solve_newton<NT>(m, s);
+  if constexpr (NT == 64 && KS::MAXEFC <= 64)
+    r_solve_newton(m, s); /* compact tier: register-resident (ur3e_wave_r.h) */
+  else
+    w_solve_newton<NT>(m, s);
   WT(15);
 }
 

@@ -1,0 +1,507 @@
+/*
+ * ur3e_wave_r.h — register-resident Newton solver for the compact tier
+ * (one 64-lane wavefront per env, nefc <= 64, nv <= K_NV <= 64).
+ *
+ * Same algorithm and the same floating-point operation order as w_solve_newton
+ * (ur3e_wave.h) and the oracle's newton solver (oracle/ur3e_oracle.c), laid out
+ * for the wavefront instead of LDS round trips:
+ *   - lane r holds constraint row r: its Jacobian row, jar, force, state, cost
+ *     terms; cone rows get their first row's zone/forces by a lane shuffle;
+ *   - lane k holds dof k: qacc, Ma, grad, search, and row k of the Hessian
+ *     (H build, right-looking Cholesky and the forward sweep stay in registers);
+ *   - ordered reductions (costs, line-search sums, norms, gradient sums) walk
+ *     the lanes in the oracle's order with v_readlane broadcasts;
+ *   - LDS is read only for qM rows, J columns, the cone Hessians and L^T.
+ * MuJoCo 3.3.3 semantics: engine_solver.c (mj_solNewton, Hessian/cone terms,
+ * linesearch), engine_core_constraint.c (mj_constraintUpdate) as restated in
+ * the oracle.
+ */
+#ifndef UR3E_WAVE_R_H
+#define UR3E_WAVE_R_H
+
+/* included from ur3e_wave.h (needs KSX, WD, WT) */
+
+/* broadcast lane `lane` (wave-uniform) of v to every lane */
+__device__ __forceinline__ double rl(double v, int lane) {
+  long long b = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_readlane((int)(unsigned int)(b & 0xffffffffll), lane);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo));
+}
+__device__ __forceinline__ int rli(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+/* per-lane source (ds_bpermute) */
+__device__ __forceinline__ double shf(double v, int src) {
+  long long b = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned int)(b & 0xffffffffll));
+  int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo));
+}
+__device__ __forceinline__ int shfi(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+
+/* one constraint row per lane (lanes >= nefc: typ = -1, never contribute) */
+struct RRow {
+  int typ, jj, first; /* jj: row index inside its contact, first: lane of the contact's first row */
+  double D, R, aref, floss, mu, fr0, fr1;
+  double J[K_NV];
+  double jar, Jv, force, F;
+  int st, flag;
+};
+
+template <class KS>
+WD void r_load_rows(KModel m, const KS& s, RRow& w) {
+  const int r = threadIdx.x;
+  const int nefc = s.nefc;
+  w.typ = -1; w.jj = 0; w.first = r;
+  w.D = 0; w.R = 0; w.aref = 0; w.floss = 0; w.mu = 0; w.fr0 = 0; w.fr1 = 0;
+  w.jar = 0; w.Jv = 0; w.force = 0; w.F = 0; w.st = ST_SATISFIED; w.flag = 0;
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) w.J[k] = 0;
+  if (r < nefc) {
+    w.typ = s.efc_type[r];
+    w.D = s.efc_D[r]; w.R = s.efc_R[r]; w.aref = s.efc_aref[r]; w.floss = s.efc_floss[r];
+#pragma unroll
+    for (int k = 0; k < K_NV; k++) w.J[k] = s.efc_J[r][k];
+    if (w.typ != CN_EQUALITY && w.typ != CN_FRICTION_DOF && w.typ != CN_LIMIT_JOINT) {
+      int c = s.efc_id[r];
+      int i0 = s.con_efc[c];
+      int p = s.con_cpair[c];
+      w.first = i0; w.jj = r - i0;
+      w.mu = s.con_mu[c];
+      w.fr0 = m->cpair_friction[p][0];
+      w.fr1 = m->cpair_friction[p][1];
+    }
+  }
+}
+
+/* mj_constraintUpdate per row (w_constraint_update) */
+WD void r_constraint_update(RRow& w) {
+  const double jar = w.jar, D = w.D, R = w.R;
+  /* contact cone: computed on every lane (uniform shuffles), used by contact lanes */
+  double jar1 = shf(jar, threadIdx.x + 1), jar2 = shf(jar, threadIdx.x + 2);
+  double mu = w.mu;
+  double U0 = jar * mu, U1 = jar1 * w.fr0, U2 = jar2 * w.fr1;
+  double N = U0;
+  double T2 = 0;
+  T2 += U1 * U1;
+  T2 += U2 * U2;
+  double T = sqrt(T2);
+  int z;
+  if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
+  else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
+  else z = 2;
+  double Dm = D / (mu * mu * (1 + mu * mu));
+  double NT_ = N - mu * T;
+  double Fm = 0.5 * Dm * NT_ * NT_;
+  double f0 = -Dm * NT_ * mu;
+  double f1 = Dm * NT_ * mu * U1 / T * w.fr0;
+  double f2 = Dm * NT_ * mu * U2 / T * w.fr1;
+  int zs = shfi(z, w.first);
+  double f1s = shf(f1, w.first), f2s = shf(f2, w.first);
+  const int t = w.typ;
+  if (t == CN_EQUALITY) {
+    w.force = -D * jar;
+    w.F = 0.5 * D * jar * jar; w.flag = 1;
+    w.st = ST_QUADRATIC;
+  } else if (t == CN_FRICTION_DOF) {
+    double fl = w.floss;
+    if (jar <= -R * fl) {
+      w.force = fl;
+      w.F = -0.5 * R * fl * fl - fl * jar;
+      w.st = ST_LINEARNEG;
+    } else if (jar >= R * fl) {
+      w.force = -fl;
+      w.F = -0.5 * R * fl * fl + fl * jar;
+      w.st = ST_LINEARPOS;
+    } else {
+      w.force = -D * jar;
+      w.F = 0.5 * D * jar * jar;
+      w.st = ST_QUADRATIC;
+    }
+    w.flag = 1;
+  } else if (t == CN_LIMIT_JOINT) {
+    if (jar >= 0) {
+      w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
+    } else {
+      w.force = -D * jar;
+      w.F = 0.5 * D * jar * jar; w.flag = 1;
+      w.st = ST_QUADRATIC;
+    }
+  } else if (t >= 0) {
+    if (zs == 0) {
+      w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
+    } else if (zs == 1) {
+      w.force = -D * jar;
+      w.F = 0.5 * D * jar * jar;
+      w.flag = 1;
+      w.st = ST_QUADRATIC;
+    } else {
+      w.st = ST_CONE;
+      if (w.jj == 0) { w.F = Fm; w.flag = 1; w.force = f0; }
+      else if (w.jj == 1) { w.flag = 0; w.force = f1s; }
+      else { w.flag = 0; w.force = f2s; }
+    }
+  } else {
+    w.flag = 0; w.force = 0; w.st = ST_SATISFIED;
+  }
+}
+
+/* uniform copy of a dof vector held one element per lane */
+WD void r_bcast(double v, int nv, double out[K_NV]) {
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) out[k] = k < nv ? rl(v, k) : 0.0;
+}
+
+/* w_eval_state: Ma (lane k), jar/force/cost terms (lane r), gauss and cost (uniform) */
+template <class KS>
+WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
+                     double& cost) {
+  const int lane = threadIdx.x;
+  const int nv = m->nv, nefc = s.nefc;
+  double qv[K_NV];
+  r_bcast(qacc, nv, qv);
+  {
+    double v = 0;
+    const int row = lane < nv ? lane : 0;
+#pragma unroll
+    for (int j = 0; j < K_NV; j++)
+      if (j < nv) v += s.qM[row][j] * qv[j];
+    Ma = v;
+  }
+  {
+    double v = 0;
+#pragma unroll
+    for (int k = 0; k < K_NV; k++)
+      if (k < nv) v += w.J[k] * qv[k];
+    w.jar = v - w.aref;
+  }
+  r_constraint_update(w);
+  double term = (Ma - qs) * (qacc - qas);
+  double a0 = 0, a1 = 0;
+  for (int i = 0; i < nv; i++) a0 += rl(term, i);
+  for (int i = 0; i < nefc; i++)
+    if (rli(w.flag, i)) a1 += rl(w.F, i);
+  gauss = 0.5 * a0;
+  cost = gauss + a1;
+}
+
+/* w_compute_grad: lane k: qfrc_constraint[k] = sum_i J[i][k] force[i] (row order), grad */
+template <class KS>
+WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double qs, double& qfrc_c, double& grad) {
+  const int lane = threadIdx.x;
+  const int nefc = s.nefc;
+  const int col = lane < K_NV ? lane : 0;
+  double f = 0;
+  for (int i = 0; i < nefc; i++) f += s.efc_J[i][col] * rl(w.force, i);
+  qfrc_c = f;
+  grad = Ma - qs - f;
+}
+
+/* Newton direction: H = M + J'DJ + cone terms (lane k = row k), Cholesky in registers,
+   x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
+template <class KS>
+WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
+  const int lane = threadIdx.x;
+  const int nv = m->nv, nefc = s.nefc;
+  /* cone Hessians (w_hessian_factor), on each contact's first-row lane */
+  {
+    double jar1 = shf(w.jar, lane + 1), jar2 = shf(w.jar, lane + 2);
+    if (w.typ >= 0 && w.typ != CN_EQUALITY && w.typ != CN_FRICTION_DOF && w.typ != CN_LIMIT_JOINT && w.jj == 0 &&
+        w.st == ST_CONE) {
+      int c = s.efc_id[lane];
+      double mu = w.mu;
+      double U[3], sc[3];
+      sc[0] = mu;
+      U[0] = w.jar * mu;
+      sc[1] = w.fr0; U[1] = jar1 * sc[1];
+      sc[2] = w.fr1; U[2] = jar2 * sc[2];
+      double T2 = 0;
+      for (int j = 1; j < 3; j++) T2 += U[j] * U[j];
+      double T = sqrt(T2);
+      double N = U[0];
+      double Dm = w.D / (mu * mu * (1 + mu * mu));
+      double Hc[3][3];
+      Hc[0][0] = 1;
+      for (int j = 1; j < 3; j++) {
+        Hc[0][j] = -mu * U[j] / T;
+        Hc[j][0] = Hc[0][j];
+      }
+      double muNT = mu * N / T;
+      for (int j = 1; j < 3; j++)
+        for (int k = 1; k < 3; k++) Hc[j][k] = (j == k ? mu * mu - muNT : 0.0) + muNT * U[j] * U[k] / T2;
+      for (int j = 0; j < 3; j++)
+        for (int k = 0; k < 3; k++) s.con_Hc[c][3 * j + k] = Hc[j][k] * Dm * sc[j] * sc[k];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int row = lane < nv ? lane : 0;
+  double h[K_NV];
+#pragma unroll
+  for (int c = 0; c < K_NV; c++) h[c] = s.qM[row][c];
+  for (int i = 0; i < nefc; i++) {
+    const int st = rli(w.st, i);
+    if (st == ST_QUADRATIC) {
+      double jr = s.efc_J[i][row];
+      double djr = rl(w.D, i) * jr;
+      if (jr != 0) {
+#pragma unroll
+        for (int c = 0; c < K_NV; c++) h[c] += djr * s.efc_J[i][c];
+      }
+    } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
+      const double* Hc = s.con_Hc[s.efc_id[i]];
+      double t[3];
+      for (int j = 0; j < 3; j++) {
+        double acc = 0;
+        for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[i + k][row];
+        t[j] = acc;
+      }
+#pragma unroll
+      for (int c = 0; c < K_NV; c++) {
+        double acc = 0;
+        for (int j = 0; j < 3; j++) acc += s.efc_J[i + j][c] * t[j];
+        h[c] += acc;
+      }
+    }
+  }
+  /* right-looking Cholesky, lane = row; element (i,k) gets -= L[i][j] L[k][j] for j = 0,1,...
+     (the oracle's left-looking order) */
+  double diag[K_NV];
+#pragma unroll
+  for (int j = 0; j < K_NV; j++) {
+    if (j < nv) {
+      double sum = rl(h[j], j);
+      if (sum < K_MINVAL) sum = K_MINVAL;
+      double ljj = sqrt(sum);
+      diag[j] = ljj;
+      if (lane > j) h[j] = h[j] / ljj;
+      if (lane == j) h[j] = ljj;
+#pragma unroll
+      for (int k = j + 1; k < K_NV; k++) {
+        if (k < nv) {
+          double lkj = rl(h[j], k);
+          if (lane >= k) h[k] -= h[j] * lkj;
+        }
+      }
+    }
+  }
+  /* forward: L y = grad (x[k] = tmp[k] / L[k][k]; tmp[i] -= L[i][k] x[k], i > k) */
+  double tmp = grad;
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) {
+    if (k < nv) {
+      double xk = rl(tmp, k) / diag[k];
+      if (lane == k) tmp = xk;
+      else if (lane > k) tmp -= h[k] * xk;
+    }
+  }
+  /* L^T via LDS (H storage; nothing else reads it during the solve) */
+  if (lane < nv) {
+#pragma unroll
+    for (int c = 0; c < K_NV; c++) s.H[lane][c] = h[c];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  double lt[K_NV];
+#pragma unroll
+  for (int i = 0; i < K_NV; i++) lt[i] = s.H[i][row];
+  /* backward: L' x = y (x[i] = tmp[i] / L[i][i]; tmp[t] -= L[i][t] x[i], t < i) */
+#pragma unroll
+  for (int i = K_NV - 1; i >= 0; i--) {
+    if (i < nv) {
+      double xi = rl(tmp, i) / diag[i];
+      if (lane == i) tmp = xi;
+      else if (lane < i) tmp -= lt[i] * xi;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  return -tmp;
+}
+
+/* line-search 1-D evaluation at a (w_ls_eval): per-row terms on the row lanes, ordered sums */
+WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF, double& lsdF,
+                  double& lsd2F) {
+  const int lane = threadIdx.x;
+  const double D = w.D, R = w.R;
+  double x = w.jar + a * w.Jv;
+  double v = w.Jv;
+  /* cone terms from the contact's first row (computed everywhere, used by contact lanes) */
+  double jar1 = shf(w.jar, lane + 1), jar2 = shf(w.jar, lane + 2);
+  double Jv1 = shf(w.Jv, lane + 1), Jv2 = shf(w.Jv, lane + 2);
+  double mu = w.mu;
+  double U0 = (w.jar + a * w.Jv) * mu, V0 = w.Jv * mu;
+  double U1 = (jar1 + a * Jv1) * w.fr0, V1 = Jv1 * w.fr0;
+  double U2 = (jar2 + a * Jv2) * w.fr1, V2 = Jv2 * w.fr1;
+  double N = U0;
+  double T2 = 0;
+  T2 += U1 * U1;
+  T2 += U2 * U2;
+  double T = sqrt(T2);
+  int z;
+  if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
+  else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
+  else z = 2;
+  double Dm = D / (mu * mu * (1 + mu * mu));
+  double UV = 0, VV = 0;
+  UV += U1 * V1; VV += V1 * V1;
+  UV += U2 * V2; VV += V2 * V2;
+  double NT_ = N - mu * T;
+  double dNT = V0 - mu * UV / T;
+  double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
+  double cF = 0.5 * Dm * NT_ * NT_;
+  double cdF = Dm * NT_ * dNT;
+  double cd2F = Dm * (dNT * dNT + NT_ * d2NT);
+  int zs = shfi(z, w.first);
+  double F = 0, dF = 0, d2F = 0;
+  int flag = 0;
+  const int t = w.typ;
+  if (t == CN_EQUALITY) {
+    F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
+  } else if (t == CN_FRICTION_DOF) {
+    double fl = w.floss;
+    if (x <= -R * fl) { F = -0.5 * R * fl * fl - fl * x; dF = -fl * v; flag = 2; }
+    else if (x >= R * fl) { F = -0.5 * R * fl * fl + fl * x; dF = fl * v; flag = 2; }
+    else { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+  } else if (t == CN_LIMIT_JOINT) {
+    if (x < 0) { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+  } else if (t >= 0) {
+    if (zs == 1) {
+      F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
+    } else if (zs == 2 && w.jj == 0) {
+      F = cF; dF = cdF; d2F = cd2F; flag = 1;
+    }
+  }
+  double aF = gauss + a * g1 + 0.5 * a * a * g2;
+  double adF = g1 + a * g2;
+  double ad2F = g2;
+  for (int i = 0; i < nefc; i++) {
+    int f = rli(flag, i);
+    if (f) {
+      aF += rl(F, i);
+      adF += rl(dF, i);
+      if (f == 1) ad2F += rl(d2F, i);
+    }
+  }
+  lsF = aF; lsdF = adF; lsd2F = ad2F;
+}
+
+/* w_line_search: returns alpha (uniform); Jv on the row lanes */
+template <class KS>
+WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma, double qs, double gauss,
+                        double scale) {
+  const int lane = threadIdx.x;
+  const int nv = m->nv, nefc = s.nefc;
+  double sv[K_NV];
+  r_bcast(search, nv, sv);
+  double sn = 0;
+  for (int k = 0; k < nv; k++) sn += sv[k] * sv[k];
+  double snorm = sqrt(sn);
+  double Mv;
+  {
+    double v = 0;
+    const int row = lane < nv ? lane : 0;
+#pragma unroll
+    for (int j = 0; j < K_NV; j++)
+      if (j < nv) v += s.qM[row][j] * sv[j];
+    Mv = v;
+  }
+  {
+    double v = 0;
+#pragma unroll
+    for (int k = 0; k < K_NV; k++)
+      if (k < nv) v += w.J[k] * sv[k];
+    w.Jv = v;
+  }
+  if (snorm < K_MINVAL) return 0;
+  double t1 = search * (Ma - qs), t2 = search * Mv;
+  double g1 = 0, g2 = 0;
+  for (int k = 0; k < nv; k++) {
+    g1 += rl(t1, k);
+    g2 += rl(t2, k);
+  }
+  double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
+  double f0, d0, h0;
+  r_ls_eval(w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
+  if (d0 >= 0) return 0;
+  double lo = 0.0, dlo = d0, hlo = h0;
+  double hi = -1.0, dhi = 0, hhi = 0;
+  double bestA = 0.0, bestF = f0;
+  double a = -d0 / h0;
+  for (int it = 0; it < m->ls_iterations; it++) {
+    double f, df, d2f;
+    r_ls_eval(w, nefc, a, gauss, g1, g2, f, df, d2f);
+    if (f < bestF) { bestF = f; bestA = a; }
+    if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
+    if (df < 0) { lo = a; dlo = df; hlo = d2f; }
+    else { hi = a; dhi = df; hhi = d2f; }
+    double na;
+    if (hi < 0) {
+      na = a - df / d2f;
+      if (!(na > a)) na = 2 * a;
+    } else {
+      double c1 = lo - dlo / hlo;
+      double c2 = hi - dhi / hhi;
+      if (c1 > lo && c1 < hi) na = c1;
+      else if (c2 > lo && c2 < hi) na = c2;
+      else na = 0.5 * (lo + hi);
+    }
+    a = na;
+  }
+  return bestA;
+}
+
+/* w_solve_newton for the compact tier; leaves s.qacc and s.qfrc_constraint */
+template <class KS>
+WD void r_solve_newton(KModel m, KS& s) {
+  const int lane = threadIdx.x;
+  const int nv = m->nv;
+  if (s.nefc == 0) {
+    if (lane < nv) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_constraint[lane] = 0; }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    return;
+  }
+  const double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  const int k = lane < nv ? lane : 0;
+  const double qs = s.qfrc_smooth[k], qas = s.qacc_smooth[k];
+  double qacc = lane < nv ? s.warm[k] : 0.0;
+  RRow w;
+  r_load_rows(m, s, w);
+  double Ma, gauss, cost;
+  r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
+  const double cost_ws = cost;
+  r_eval_state(m, s, w, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost);
+  const double cost_sm = cost;
+  if (cost_ws > cost_sm) {
+    qacc = lane < nv ? qas : 0.0;
+  } else {
+    r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
+  }
+  double qfrc_c, grad;
+  r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
+  WT(9);
+  double search = r_direction(m, s, w, grad);
+  WT(11);
+  for (int iter = 0; iter < m->iterations; iter++) {
+    double alpha = r_line_search(m, s, w, search, Ma, qs, gauss, scale);
+    WT(13);
+    if (alpha == 0) break;
+    qacc += alpha * search;
+    double oldcost = cost;
+    r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
+    r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
+    WT(14);
+    double gn = 0;
+    for (int i = 0; i < nv; i++) gn += rl(grad, i) * rl(grad, i);
+    double improvement = scale * (oldcost - cost);
+    double gradient = scale * sqrt(gn);
+    if (improvement < m->tolerance || gradient < m->tolerance) break;
+    search = r_direction(m, s, w, grad);
+    WT(11);
+  }
+  if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+#endif /* UR3E_WAVE_R_H */
