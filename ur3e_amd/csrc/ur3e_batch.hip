@@ -1046,9 +1046,14 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
     HIPCHK(hipMemsetAsync(b->d_ovf_count, 0, sizeof(int), st));
-    hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
-                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_count);
+    if (b->host_model.nv == K_NV) /* main.xml: dof loops specialised at compile time */
+      hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
+                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf_list, b->d_ovf_count);
+    else
+      hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                         d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                         b->d_ovf_count);
     int grid = b->n < 512 ? b->n : 512;
     hipLaunchKernelGGL(w_env_step_list<128>, dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,

@@ -48,8 +48,9 @@ struct KPlan {
 #define G_LIMIT 3
 #define G_CONTACT 4
 
-template <int MC, int ME>
+template <int MC, int ME, int NVC = 0>
 struct KSX {
+  static constexpr int NV = NVC;    /* > 0: kernel specialised for a model with exactly NVC dofs */
   static constexpr int MAXCON = MC; /* contacts this tier holds */
   static constexpr int MAXEFC = ME; /* constraint rows this tier holds */
   static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
@@ -112,6 +113,9 @@ typedef KSX<K_MAXCON, K_MAXEFC> KSL;
 #define W_SMALL_MAXEFC 44
 #endif
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
+/* compact tier specialised for nv == K_NV (main.xml): every dof loop has a compile-time trip count */
+typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, K_NV> KSS_NV;
+#define NVOF(KS, m) ((KS::NV) ? (KS::NV) : (m)->nv)
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
    wave's LDS instructions issue and complete in program order, so cross-lane LDS hand-offs only
@@ -335,7 +339,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
 template <int NT, class KS>
 WD void w_crb(KModel m, KS& s) {
   const int tid = threadIdx.x;
-  const int nb = m->nbody, nv = m->nv;
+  const int nb = m->nbody, nv = NVOF(KS, m);
   for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
   for (int e = tid; e < nv * nv; e += NT) s.qM[e / nv][e % nv] = 0;
   SYNC();
@@ -502,7 +506,7 @@ KD void w_jacp_col(KModel m, const KPlan* __restrict__ pl, const KS& s, int body
 template <class KS>
 KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double* simp, double pos, double margin,
                         double diag, int friction_row) {
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   double vel = 0;
   for (int k = 0; k < nv; k++) vel += s.efc_J[r][k] * s.qvel[k];
   double imp = k_get_impedance(simp, pos, margin);
@@ -531,7 +535,7 @@ KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double
 template <int NT, class KS>
 WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   /* lane 0 lays out the row groups in oracle order; a group that does not fit stops the layout */
   if (tid == 0) {
     int nrow = 0, ng = 0, stop = 0;
@@ -747,7 +751,7 @@ WD void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
 template <int NT, class KS>
 WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
-  const int nb = m->nbody, nv = m->nv;
+  const int nb = m->nbody, nv = NVOF(KS, m);
   double (*cacc)[10] = s.u.body.b10;
   double (*cfrc)[6] = s.u.body.b6;
   if (tid == 0) {
@@ -936,7 +940,7 @@ WD void w_constraint_update(KModel m, KS& s) {
 template <int NT, class KS>
 WD void w_eval_state(KModel m, KS& s, const double* qacc) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   for (int i = tid; i < nv + s.nefc; i += NT) {
     if (i < nv) {
       double v = 0;
@@ -973,7 +977,7 @@ WD void w_eval_state(KModel m, KS& s, const double* qacc) {
 template <int NT, class KS>
 WD void w_compute_grad(KModel m, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   if (tid < nv) {
     int k = tid;
     double f = 0;
@@ -987,7 +991,7 @@ WD void w_compute_grad(KModel m, KS& s) {
 template <int NT, class KS>
 WD void w_hessian_factor(KModel m, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   /* cone Hessians (middle zone), one lane per contact */
   for (int c = tid; c < s.ncon; c += NT) {
     int i = s.con_efc[c];
@@ -1081,7 +1085,7 @@ WD void w_hessian_factor(KModel m, KS& s) {
 template <int NT, class KS>
 WD void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   if (tid < nv) s.tmpv[tid] = b[tid];
   SYNC();
   for (int k = 0; k < nv; k++) {
@@ -1186,7 +1190,7 @@ WD void w_ls_eval(KModel m, KS& s, double a) {
 template <int NT, class KS>
 WD double w_line_search(KModel m, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   if (tid == 0) {
     double sn = 0;
     for (int k = 0; k < nv; k++) sn += s.search[k] * s.search[k];
@@ -1248,7 +1252,7 @@ WD double w_line_search(KModel m, KS& s) {
 template <int NT, class KS>
 WD void w_solve_newton(KModel m, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   if (s.nefc == 0) {
     if (tid < nv) { s.qacc[tid] = s.qacc_smooth[tid]; s.qfrc_constraint[tid] = 0; }
     SYNC();
@@ -1311,17 +1315,20 @@ WD void w_solve_newton(KModel m, KS& s) {
 template <int NT, class KS>
 WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
+  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64); /* compact tier: ur3e_wave_r.h */
   WT_START();
   w_kinematics<NT>(m, pl, s);
   WT(0);
   w_com_pos<NT>(m, pl, s);
   WT(1);
   w_crb<NT>(m, s);
-  for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
-  SYNC();
-  WT(2);
-  w_factor_tree<NT>(m, pl, s.H, s.LDinv, s.tmpv);
+  if constexpr (!REG) {
+    for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
+    SYNC();
+    WT(2);
+    w_factor_tree<NT>(m, pl, s.H, s.LDinv, s.tmpv);
+  }
   WT(3);
   w_collision<NT>(m, s);
   WT(4);
@@ -1333,10 +1340,16 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   WT(6);
   w_rne_passive<NT>(m, pl, s);
   WT(7);
-  w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+  if constexpr (REG) {
+    double x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0);
+    if (tid < nv) s.qacc_smooth[tid] = x;
+    SYNC();
+  } else {
+    w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+  }
   WT(8);
-  if constexpr (NT == 64 && KS::MAXEFC <= 64)
-    r_solve_newton(m, s); /* compact tier: register-resident (ur3e_wave_r.h) */
+  if constexpr (REG)
+    r_solve_newton(m, s);
   else
     w_solve_newton<NT>(m, s);
   WT(15);
@@ -1345,7 +1358,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
 template <int NT, class KS>
 WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
-  const int nq = m->nq, nv = m->nv;
+  const int nq = m->nq, nv = NVOF(KS, m);
   if (tid == 0) {
     int bad = 0;
     for (int k = 0; k < nq; k++) bad |= k_is_bad(s.qpos[k]);
@@ -1378,7 +1391,14 @@ WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
   /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
   int damped = 0;
   for (int k = 0; k < nv; k++) damped |= m->dof_damping[k] > 0;
-  if (damped) {
+  if (!damped) {
+    if (tid < nv) s.xv[tid] = s.qacc[tid];
+    SYNC();
+  } else if constexpr (NT == 64 && KS::MAXEFC <= 64) {
+    double x = r_tree_solve(m, pl, s, true, tid < nv ? s.qfrc_smooth[tid] + s.qfrc_constraint[tid] : 0.0);
+    if (tid < nv) s.xv[tid] = x;
+    SYNC();
+  } else {
     for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
     SYNC();
     if (tid < nv) {
@@ -1388,9 +1408,6 @@ WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     SYNC();
     w_factor_tree<NT>(m, pl, s.H, s.grad, s.tmpv);
     w_solve_tree<NT>(m, pl, s.H, s.grad, s.xv, s.fv);
-  } else {
-    if (tid < nv) s.xv[tid] = s.qacc[tid];
-    SYNC();
   }
   WT(16);
   double h = m->timestep;

@@ -156,7 +156,7 @@ template <class KS>
 WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
                      double& cost) {
   const int lane = threadIdx.x;
-  const int nv = m->nv, nefc = s.nefc;
+  const int nv = NVOF(KS, m), nefc = s.nefc;
   double qv[K_NV];
   r_bcast(qacc, nv, qv);
   {
@@ -177,9 +177,14 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
   r_constraint_update(w);
   double term = (Ma - qs) * (qacc - qas);
   double a0 = 0, a1 = 0;
-  for (int i = 0; i < nv; i++) a0 += rl(term, i);
-  for (int i = 0; i < nefc; i++)
-    if (rli(w.flag, i)) a1 += rl(w.F, i);
+#pragma unroll
+  for (int i = 0; i < K_NV; i++)
+    if (i < nv) a0 += rl(term, i);
+  for (int i = 0; i < nefc; i++) {
+    double f = rl(w.F, i);
+    double n = a1 + f;
+    a1 = rli(w.flag, i) ? n : a1; /* select, not a skipped add: -0 stays -0 as in the oracle */
+  }
   gauss = 0.5 * a0;
   cost = gauss + a1;
 }
@@ -201,7 +206,7 @@ WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double q
 template <class KS>
 WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
   const int lane = threadIdx.x;
-  const int nv = m->nv, nefc = s.nefc;
+  const int nv = NVOF(KS, m), nefc = s.nefc;
   /* cone Hessians (w_hessian_factor), on each contact's first-row lane */
   {
     double jar1 = shf(w.jar, lane + 1), jar2 = shf(w.jar, lane + 2);
@@ -238,14 +243,31 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
   double h[K_NV];
 #pragma unroll
   for (int c = 0; c < K_NV; c++) h[c] = s.qM[row][c];
+  /* rows in oracle order; row i's broadcast J row is loaded one iteration ahead */
+  double jn[K_NV], jrn = 0;
+  if (nefc > 0) {
+#pragma unroll
+    for (int c = 0; c < K_NV; c++) jn[c] = s.efc_J[0][c];
+    jrn = s.efc_J[0][row];
+  }
   for (int i = 0; i < nefc; i++) {
+    double jc[K_NV];
+#pragma unroll
+    for (int c = 0; c < K_NV; c++) jc[c] = jn[c];
+    const double jr = jrn;
+    if (i + 1 < nefc) {
+#pragma unroll
+      for (int c = 0; c < K_NV; c++) jn[c] = s.efc_J[i + 1][c];
+      jrn = s.efc_J[i + 1][row];
+    }
     const int st = rli(w.st, i);
     if (st == ST_QUADRATIC) {
-      double jr = s.efc_J[i][row];
-      double djr = rl(w.D, i) * jr;
-      if (jr != 0) {
+      const double djr = rl(w.D, i) * jr;
+      const bool use = jr != 0;
 #pragma unroll
-        for (int c = 0; c < K_NV; c++) h[c] += djr * s.efc_J[i][c];
+      for (int c = 0; c < K_NV; c++) {
+        double n = h[c] + djr * jc[c];
+        h[c] = use ? n : h[c];
       }
     } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
       const double* Hc = s.con_Hc[s.efc_id[i]];
@@ -263,6 +285,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
       }
     }
   }
+  WT(10);
   /* right-looking Cholesky, lane = row; element (i,k) gets -= L[i][j] L[k][j] for j = 0,1,...
      (the oracle's left-looking order) */
   double diag[K_NV];
@@ -284,6 +307,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
       }
     }
   }
+  WT(12);
   /* forward: L y = grad (x[k] = tmp[k] / L[k][k]; tmp[i] -= L[i][k] x[k], i > k) */
   double tmp = grad;
 #pragma unroll
@@ -294,6 +318,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
       else if (lane > k) tmp -= h[k] * xk;
     }
   }
+  WT(18);
   /* L^T via LDS (H storage; nothing else reads it during the solve) */
   if (lane < nv) {
 #pragma unroll
@@ -375,12 +400,11 @@ WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, do
   double adF = g1 + a * g2;
   double ad2F = g2;
   for (int i = 0; i < nefc; i++) {
-    int f = rli(flag, i);
-    if (f) {
-      aF += rl(F, i);
-      adF += rl(dF, i);
-      if (f == 1) ad2F += rl(d2F, i);
-    }
+    const int f = rli(flag, i);
+    double nF = aF + rl(F, i), ndF = adF + rl(dF, i), nd2F = ad2F + rl(d2F, i);
+    aF = f ? nF : aF;
+    adF = f ? ndF : adF;
+    ad2F = f == 1 ? nd2F : ad2F;
   }
   lsF = aF; lsdF = adF; lsd2F = ad2F;
 }
@@ -390,11 +414,13 @@ template <class KS>
 WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma, double qs, double gauss,
                         double scale) {
   const int lane = threadIdx.x;
-  const int nv = m->nv, nefc = s.nefc;
+  const int nv = NVOF(KS, m), nefc = s.nefc;
   double sv[K_NV];
   r_bcast(search, nv, sv);
   double sn = 0;
-  for (int k = 0; k < nv; k++) sn += sv[k] * sv[k];
+#pragma unroll
+  for (int k = 0; k < K_NV; k++)
+    if (k < nv) sn += sv[k] * sv[k];
   double snorm = sqrt(sn);
   double Mv;
   {
@@ -415,9 +441,12 @@ WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma
   if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
   double g1 = 0, g2 = 0;
-  for (int k = 0; k < nv; k++) {
-    g1 += rl(t1, k);
-    g2 += rl(t2, k);
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) {
+    if (k < nv) {
+      g1 += rl(t1, k);
+      g2 += rl(t2, k);
+    }
   }
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
@@ -454,7 +483,7 @@ WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma
 template <class KS>
 WD void r_solve_newton(KModel m, KS& s) {
   const int lane = threadIdx.x;
-  const int nv = m->nv;
+  const int nv = NVOF(KS, m);
   if (s.nefc == 0) {
     if (lane < nv) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_constraint[lane] = 0; }
     __builtin_amdgcn_wave_barrier();
@@ -492,7 +521,9 @@ WD void r_solve_newton(KModel m, KS& s) {
     r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
     WT(14);
     double gn = 0;
-    for (int i = 0; i < nv; i++) gn += rl(grad, i) * rl(grad, i);
+#pragma unroll
+    for (int i = 0; i < K_NV; i++)
+      if (i < nv) gn += rl(grad, i) * rl(grad, i);
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
@@ -502,6 +533,84 @@ WD void r_solve_newton(KModel m, KS& s) {
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+}
+
+/* mj_factorI + mj_solveLD on A = qM (+ h*damping on the diagonal when `damped`), compact tier:
+   the reverse tree LDL' runs in registers in COLUMN layout (lane j holds A[i][j] for all i), so
+   every cross-lane operand is a readlane of a constant register index; the forward substitution
+   needs rows and gets them through one LDS transpose (s.H).  Same element update order as
+   w_factor_tree / w_solve_tree.  Returns x = A^-1 b on lane t (< nv). */
+template <class KS>
+WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool damped, double b) {
+  const int lane = threadIdx.x;
+  const int nv = NVOF(KS, m);
+  const int col = lane < nv ? lane : 0;
+  double a[K_NV];
+#pragma unroll
+  for (int i = 0; i < K_NV; i++) a[i] = s.qM[i][col];
+  if (damped) {
+#pragma unroll
+    for (int i = 0; i < K_NV; i++)
+      if (lane == i && i < nv) a[i] += m->timestep * m->dof_damping[i];
+  }
+  const unsigned int lbit = lane < 32 ? (1u << lane) : 0u;
+#pragma unroll
+  for (int k = K_NV - 1; k >= 0; k--) {
+    if (k < nv) {
+      double akk = rl(a[k], k);
+      if (akk < K_MINVAL) akk = K_MINVAL;
+      if (lane == k) a[k] = akk;
+      const unsigned int am = pl->dof_anc_mask[k];
+      if (am) {
+        double tmp = a[k] / akk; /* lane i in anc(k): A[k][i] / A[k][k] */
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+          if ((am >> i) & 1u) {
+            double ti = rl(tmp, i);
+            if ((am & lbit) && lane <= i) a[i] -= a[k] * ti;
+          }
+        }
+        if (am & lbit) a[k] = tmp;
+      }
+    }
+  }
+  double dg = 1.0;
+#pragma unroll
+  for (int i = 0; i < K_NV; i++)
+    if (lane == i && i < nv) dg = a[i];
+  const double dinv = 1.0 / dg;
+  double x = lane < nv ? b : 0.0;
+#pragma unroll
+  for (int i = K_NV - 1; i >= 0; i--) {
+    if (i < nv) {
+      const unsigned int am = pl->dof_anc_mask[i];
+      if (am) {
+        double xi = rl(x, i);
+        if (am & lbit) x -= a[i] * xi;
+      }
+    }
+  }
+  if (lane < nv) x *= dinv;
+  if (lane < nv) {
+#pragma unroll
+    for (int i = 0; i < K_NV; i++) s.H[i][lane] = a[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const unsigned int myam = lane < nv ? pl->dof_anc_mask[lane] : 0u;
+  double r[K_NV];
+#pragma unroll
+  for (int j = 0; j < K_NV; j++) r[j] = s.H[col][j];
+#pragma unroll
+  for (int j = 0; j < K_NV; j++) {
+    if (j < nv) {
+      double xj = rl(x, j);
+      if ((myam >> j) & 1u) x -= r[j] * xj;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  return x;
 }
 
 #endif /* UR3E_WAVE_R_H */
