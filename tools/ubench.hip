@@ -37,6 +37,22 @@ __global__ void kb(int which, double* out, unsigned long long* cyc, int reps) {
       for (int i = 0; i < 100; i++) v = sqrt(v + 1.0);
     } else if (which == 3) {
       for (int i = 0; i < 100; i++) v = 3.0 / (v + 1.0);
+    } else if (which == 6) {
+      double a0 = v, a1 = v + 1, a2 = v + 2, a3 = v + 3, a4 = v + 4, a5 = v + 5, a6 = v + 6, a7 = v + 7;
+      for (int i = 0; i < 125; i++) {
+        a0 = a0 * 1.0000001; a1 = a1 * 1.0000001; a2 = a2 * 1.0000001; a3 = a3 * 1.0000001;
+        a4 = a4 * 1.0000001; a5 = a5 * 1.0000001; a6 = a6 * 1.0000001; a7 = a7 * 1.0000001;
+      }
+      v = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    } else if (which == 7) {
+      for (int i = 0; i < 1000; i++) v = v * 1.0000001;
+    } else if (which == 8) {
+      float f0 = v, f1 = v + 1, f2 = v + 2, f3 = v + 3, f4 = v + 4, f5 = v + 5, f6 = v + 6, f7 = v + 7;
+      for (int i = 0; i < 125; i++) {
+        f0 = f0 * 1.0000001f; f1 = f1 * 1.0000001f; f2 = f2 * 1.0000001f; f3 = f3 * 1.0000001f;
+        f4 = f4 * 1.0000001f; f5 = f5 * 1.0000001f; f6 = f6 * 1.0000001f; f7 = f7 * 1.0000001f;
+      }
+      v = f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7;
     } else if (which == 4) {
 #pragma unroll
       for (int j = 0; j < NV; j++) {
@@ -86,8 +102,9 @@ int main() {
   hipMalloc(&out, sizeof(double) * 64 * 4096);
   hipMalloc(&cyc, sizeof(unsigned long long) * 4096);
   const char* names[] = {"fp64 add chain x1000", "rl-sum 20 lanes x50", "sqrt chain x100", "div chain x100",
-                         "cholesky20 readlane", "cholesky20 lds-bcast"};
-  for (int which = 0; which < 6; which++) {
+                         "cholesky20 readlane", "cholesky20 lds-bcast", "fp64 mul 8 indep x125", "fp64 mul dep x1000",
+                         "fp32 mul 8 indep x125"};
+  for (int which = 0; which < 9; which++) {
     for (int grid : {1, 1024}) {
       int reps = 4;
       hipLaunchKernelGGL(kb, dim3(grid), dim3(64), 0, 0, which, out, cyc, 1);

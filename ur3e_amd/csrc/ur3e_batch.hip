@@ -924,6 +924,8 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
   }
   for (int v = 0; v < m->nv; v++)
     if (m->dof_frictionloss[v] > 0) pl->floss_dof[pl->nfloss++] = v;
+  for (int b = 0; b < m->nbody; b++)
+    if (m->body_jntnum[b] > pl->max_jntnum) pl->max_jntnum = m->body_jntnum[b];
 }
 
 extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,

@@ -39,6 +39,7 @@ struct KPlan {
   int nfloss;
   int floss_dof[K_NV];
   int neq_rows;
+  int max_jntnum; /* joints on the busiest body (the compact tier's body passes need <= 1) */
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -158,6 +159,8 @@ __device__ unsigned long long ur3e_stage_calls[32];
   do {             \
   } while (0)
 #endif
+
+#include "ur3e_wave_r.h"
 
 /* ================================================================== */
 /* kinematics (level-parallel over bodies)                             */
@@ -754,6 +757,10 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int nb = m->nbody, nv = NVOF(KS, m);
   double (*cacc)[10] = s.u.body.b10;
   double (*cfrc)[6] = s.u.body.b6;
+  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64);
+  if constexpr (REG) {
+    r_cfrc(m, s); /* cacc came from r_vel_acc */
+  } else {
   if (tid == 0) {
     cacc[0][0] = cacc[0][1] = cacc[0][2] = 0;
     cacc[0][3] = -m->gravity[0]; cacc[0][4] = -m->gravity[1]; cacc[0][5] = -m->gravity[2];
@@ -788,6 +795,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   SYNC();
+  }
   if (tid < nv) {
     int v = tid;
     s.qfrc_bias[v] = k_dot6(s.cdof[v], cfrc[m->dof_bodyid[v]]);
@@ -1307,8 +1315,6 @@ WD void w_solve_newton(KModel m, KS& s) {
   }
 }
 
-#include "ur3e_wave_r.h"
-
 /* ================================================================== */
 /* forward / step                                                      */
 /* ================================================================== */
@@ -1318,7 +1324,12 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64); /* compact tier: ur3e_wave_r.h */
   WT_START();
-  w_kinematics<NT>(m, pl, s);
+  if constexpr (REG) {
+    if (pl->max_jntnum <= 1) r_kinematics(m, pl, s);
+    else w_kinematics<NT>(m, pl, s);
+  } else {
+    w_kinematics<NT>(m, pl, s);
+  }
   WT(0);
   w_com_pos<NT>(m, pl, s);
   WT(1);
@@ -1336,7 +1347,8 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   w_make_constraint<NT>(m, pl, s);
   WT(5);
   if (KS::BAIL && s.ovf) return;
-  w_com_vel<NT>(m, pl, s);
+  if constexpr (REG) r_vel_acc(m, pl, s);
+  else w_com_vel<NT>(m, pl, s);
   WT(6);
   w_rne_passive<NT>(m, pl, s);
   WT(7);

@@ -545,13 +545,20 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   const int lane = threadIdx.x;
   const int nv = NVOF(KS, m);
   const int col = lane < nv ? lane : 0;
+  /* plan masks and damping up front: one batch of scalar loads, not one wait per column */
+  unsigned int amask[K_NV];
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) amask[k] = pl->dof_anc_mask[k];
   double a[K_NV];
 #pragma unroll
   for (int i = 0; i < K_NV; i++) a[i] = s.qM[i][col];
   if (damped) {
+    const double hstep = m->timestep;
+    const double dmp = lane < nv ? m->dof_damping[col] : 0.0;
+    const double add = hstep * dmp;
 #pragma unroll
     for (int i = 0; i < K_NV; i++)
-      if (lane == i && i < nv) a[i] += m->timestep * m->dof_damping[i];
+      if (lane == i && i < nv) a[i] += add;
   }
   const unsigned int lbit = lane < 32 ? (1u << lane) : 0u;
 #pragma unroll
@@ -560,7 +567,7 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
       double akk = rl(a[k], k);
       if (akk < K_MINVAL) akk = K_MINVAL;
       if (lane == k) a[k] = akk;
-      const unsigned int am = pl->dof_anc_mask[k];
+      const unsigned int am = amask[k];
       if (am) {
         double tmp = a[k] / akk; /* lane i in anc(k): A[k][i] / A[k][k] */
 #pragma unroll
@@ -583,7 +590,7 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
 #pragma unroll
   for (int i = K_NV - 1; i >= 0; i--) {
     if (i < nv) {
-      const unsigned int am = pl->dof_anc_mask[i];
+      const unsigned int am = amask[i];
       if (am) {
         double xi = rl(x, i);
         if (am & lbit) x -= a[i] * xi;
@@ -611,6 +618,228 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   return x;
+}
+
+/* ================================================================== */
+/* body-tree passes for the compact tier (lane = body, nbody <= 64)    */
+/* ================================================================== */
+/* every per-body model constant a pass needs is loaded before its level loop, so a level
+   costs one LDS read of the parent + the arithmetic, not a chain of dependent global loads;
+   bodies carry at most one joint (KPlan.max_jntnum <= 1, checked by the caller) */
+
+/* w_kinematics (mj_kinematics) */
+template <class KS>
+WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int lane = threadIdx.x;
+  const int nb = m->nbody, nlevel = pl->nlevel;
+  const int b = lane < nb ? lane : 0;
+  const int depth = (lane < nb && lane > 0) ? pl->body_depth[b] : -1;
+  const int pid = m->body_parentid[b];
+  const int jn = m->body_jntnum[b];
+  const int jf = m->body_jntadr[b];
+  const int jfc = jn ? jf : 0;
+  const int jt = m->jnt_type[jfc];
+  const int qa = m->jnt_qposadr[jfc];
+  double bpos[3], bquat[4], jax[3], jps[3];
+  for (int c = 0; c < 3; c++) { bpos[c] = m->body_pos[b][c]; jax[c] = m->jnt_axis[jfc][c]; jps[c] = m->jnt_pos[jfc][c]; }
+  for (int c = 0; c < 4; c++) bquat[c] = m->body_quat[b][c];
+  const double q0 = m->qpos0[qa];
+  /* frames hanging off bodies: lane g < ngeom -> geom g, then sites */
+  const int ng = m->ngeom, nfr = m->ngeom + m->nsite;
+  int fb = 0;
+  double fpos[3] = {0, 0, 0}, fquat[4] = {1, 0, 0, 0};
+  if (lane < ng) {
+    fb = m->geom_bodyid[lane];
+    for (int c = 0; c < 3; c++) fpos[c] = m->geom_pos[lane][c];
+    for (int c = 0; c < 4; c++) fquat[c] = m->geom_quat[lane][c];
+  } else if (lane < nfr) {
+    const int q = lane - ng;
+    fb = m->site_bodyid[q];
+    for (int c = 0; c < 3; c++) fpos[c] = m->site_pos[q][c];
+    for (int c = 0; c < 4; c++) fquat[c] = m->site_quat[q][c];
+  }
+  /* hinge rotation of this body's joint (w_kinematics' qloc pass) */
+  double ql[4] = {1, 0, 0, 0};
+  if (depth > 0 && jn == 1 && jt != UR3E_JNT_FREE) k_axis_angle_quat(ql, jax, s.qpos[qa] - q0);
+  if (lane == 0) {
+    s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
+    s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
+    k_quat2mat(s.xmat[0], s.xquat[0]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  for (int lvl = 1; lvl <= nlevel; lvl++) {
+    if (depth == lvl) {
+      double xpos[3], xquat[4];
+      if (jn == 1 && jt == UR3E_JNT_FREE) {
+        xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
+        xquat[0] = s.qpos[qa + 3]; xquat[1] = s.qpos[qa + 4]; xquat[2] = s.qpos[qa + 5]; xquat[3] = s.qpos[qa + 6];
+        k_normalize4(xquat);
+        s.xanchor[jf][0] = xpos[0]; s.xanchor[jf][1] = xpos[1]; s.xanchor[jf][2] = xpos[2];
+        s.xaxis[jf][0] = 0; s.xaxis[jf][1] = 0; s.xaxis[jf][2] = 1;
+      } else {
+        double pm[9], pp[3], pq[4];
+        for (int c = 0; c < 9; c++) pm[c] = s.xmat[pid][c];
+        for (int c = 0; c < 3; c++) pp[c] = s.xpos[pid][c];
+        for (int c = 0; c < 4; c++) pq[c] = s.xquat[pid][c];
+        double tv[3];
+        k_mat_vec3(tv, pm, bpos);
+        xpos[0] = pp[0] + tv[0]; xpos[1] = pp[1] + tv[1]; xpos[2] = pp[2] + tv[2];
+        k_mul_quat(xquat, pq, bquat);
+        if (jn == 1) {
+          double xaxis[3], xanchor[3], vec[3];
+          k_rot_vec_quat(xaxis, jax, xquat);
+          k_rot_vec_quat(xanchor, jps, xquat);
+          xanchor[0] += xpos[0]; xanchor[1] += xpos[1]; xanchor[2] += xpos[2];
+          k_mul_quat(xquat, xquat, ql);
+          k_rot_vec_quat(vec, jps, xquat);
+          xpos[0] = xanchor[0] - vec[0]; xpos[1] = xanchor[1] - vec[1]; xpos[2] = xanchor[2] - vec[2];
+          for (int c = 0; c < 3; c++) { s.xanchor[jf][c] = xanchor[c]; s.xaxis[jf][c] = xaxis[c]; }
+        }
+      }
+      k_normalize4(xquat);
+      for (int c = 0; c < 3; c++) s.xpos[lane][c] = xpos[c];
+      for (int c = 0; c < 4; c++) s.xquat[lane][c] = xquat[c];
+      double xm[9];
+      k_quat2mat(xm, xquat);
+      for (int c = 0; c < 9; c++) s.xmat[lane][c] = xm[c];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (lane < nfr) {
+    double bp[3], bq[4], bm[9], op[3], om[9];
+    for (int c = 0; c < 3; c++) bp[c] = s.xpos[fb][c];
+    for (int c = 0; c < 4; c++) bq[c] = s.xquat[fb][c];
+    for (int c = 0; c < 9; c++) bm[c] = s.xmat[fb][c];
+    k_local2global(op, om, bp, bq, bm, fpos, fquat);
+    if (lane < ng) {
+      for (int c = 0; c < 3; c++) s.geom_xpos[lane][c] = op[c];
+      for (int c = 0; c < 9; c++) s.geom_xmat[lane][c] = om[c];
+    } else {
+      for (int c = 0; c < 3; c++) s.site_xpos[lane - ng][c] = op[c];
+      for (int c = 0; c < 9; c++) s.site_xmat[lane - ng][c] = om[c];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+/* w_com_vel fused with the forward (cacc) pass of w_rne_passive: both only need the parent's
+   values, so one level sweep produces cvel, cdof_dot and cacc */
+template <class KS>
+WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int lane = threadIdx.x;
+  const int nb = m->nbody, nlevel = pl->nlevel;
+  const int b = lane < nb ? lane : 0;
+  const int depth = (lane < nb && lane > 0) ? pl->body_depth[b] : -1;
+  const int pid = m->body_parentid[b];
+  const int bda = m->body_dofadr[b];
+  const int bdn = m->body_dofnum[b];
+  const int jt = bdn ? m->jnt_type[m->dof_jntid[bda]] : UR3E_JNT_HINGE;
+  double (*cacc)[10] = s.u.body.b10;
+  /* single-dof bodies: their cdof row and qvel, loaded up front */
+  double cd[6] = {0, 0, 0, 0, 0, 0}, qv = 0;
+  if (bdn == 1) {
+    for (int r = 0; r < 6; r++) cd[r] = s.cdof[bda][r];
+    qv = s.qvel[bda];
+  }
+  if (lane == 0) {
+    for (int k = 0; k < 6; k++) s.cvel[0][k] = 0;
+    cacc[0][0] = cacc[0][1] = cacc[0][2] = 0;
+    cacc[0][3] = -m->gravity[0]; cacc[0][4] = -m->gravity[1]; cacc[0][5] = -m->gravity[2];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  for (int lvl = 1; lvl <= nlevel; lvl++) {
+    if (depth == lvl) {
+      double cv[6], ca[6];
+      for (int k = 0; k < 6; k++) { cv[k] = s.cvel[pid][k]; ca[k] = cacc[pid][k]; }
+      if (bdn == 1 && jt != UR3E_JNT_FREE) {
+        double cdd[6];
+        k_cross_motion(cdd, cv, cd);
+        for (int r = 0; r < 6; r++) cv[r] += cd[r] * qv;
+        for (int r = 0; r < 6; r++) s.cdof_dot[bda][r] = cdd[r];
+        double tmp[6] = {0, 0, 0, 0, 0, 0};
+        for (int r = 0; r < 6; r++) tmp[r] += cdd[r] * qv;
+        for (int r = 0; r < 6; r++) ca[r] = ca[r] + tmp[r];
+      } else {
+        /* general body (free joint, several dofs): w_com_vel then the cacc sum */
+        for (int j = 0; j < bdn; j++) {
+          int dof = bda + j;
+          int jtj = m->jnt_type[m->dof_jntid[dof]];
+          if (jtj == UR3E_JNT_FREE) {
+            for (int k = 0; k < 3; k++)
+              for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
+            double tmp[6] = {0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < 3; k++)
+              for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+            for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+            for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
+            for (int r = 0; r < 6; r++) tmp[r] = 0;
+            for (int k = 3; k < 6; k++)
+              for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+            for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+            j += 5;
+          } else {
+            k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
+            for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
+          }
+        }
+        double tmp[6] = {0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < bdn; j++)
+          for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+        for (int r = 0; r < 6; r++) ca[r] = ca[r] + tmp[r];
+      }
+      for (int k = 0; k < 6; k++) { s.cvel[lane][k] = cv[k]; cacc[lane][k] = ca[k]; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+/* body forces of w_rne_passive: cfrc per body, subtree sums in the oracle's order
+   (i = nb-1 .. 1, parent += child) as a readlane chain, written to LDS for qfrc_bias */
+template <class KS>
+WD void r_cfrc(KModel m, KS& s) {
+  const int lane = threadIdx.x;
+  const int nb = m->nbody;
+  double (*cacc)[10] = s.u.body.b10;
+  double (*cfrc)[6] = s.u.body.b6;
+  int par[K_NB];
+#pragma unroll
+  for (int i = 0; i < K_NB; i++) par[i] = m->body_parentid[i];
+  double f[6] = {0, 0, 0, 0, 0, 0};
+  if (lane >= 1 && lane < nb) {
+    double ci[10], ca[6], cv[6];
+    for (int k = 0; k < 10; k++) ci[k] = s.cinert[lane][k];
+    for (int k = 0; k < 6; k++) { ca[k] = cacc[lane][k]; cv[k] = s.cvel[lane][k]; }
+    double f1[6], f2[6], f3[6];
+    k_mul_inert_vec(f1, ci, ca);
+    k_mul_inert_vec(f2, ci, cv);
+    k_cross_force(f3, cv, f2);
+    for (int r = 0; r < 6; r++) f[r] = f1[r] + f3[r];
+  }
+#pragma unroll
+  for (int i = K_NB - 1; i > 0; i--) {
+    if (i < nb) {
+      const int p = par[i];
+      if (p > 0) {
+        double v[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++) v[r] = rl(f[r], i);
+        if (lane == p) {
+#pragma unroll
+          for (int r = 0; r < 6; r++) f[r] += v[r];
+        }
+      }
+    }
+  }
+  if (lane < nb) {
+    for (int r = 0; r < 6; r++) cfrc[lane][r] = lane == 0 ? 0.0 : f[r];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 
 #endif /* UR3E_WAVE_R_H */
