@@ -4,7 +4,9 @@ Workload (BASELINE.json configs[3], per GPU): `assets/main.xml` (arm + 2F-85 +
 mug, contacts on), gymnasium `ur3e-v2` step semantics (pid_task_ctrl + 2
 physics substeps + obs/reward/termination + auto-reset at T=2500), uniformly
 random task-space actions in the v2 action Box, 4096 envs per GPU.  One
-"step" = one env-step of all resident envs = one launch of k_env_step.
+"step" = one env-step of all resident envs = one ur3e_batch_step call: the
+compact-tier kernel w_env_step<64, KSS_NV> (one wavefront per env, working set
+in LDS) plus the full-capacity fallback kernel over the envs it queued.
 
 Multi-GPU: one process per GPU (torchrun), envs sharded by contiguous global
 id (weak scaling: 4096 per GPU), per-step RCCL gather of (obs, reward, done)
@@ -30,7 +32,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 ALGO_BYTES_PER_ENV_STEP = 1898
 
 
-def cpu_baseline(n_envs_sample=4096, steps=100, seed=0):
+def cpu_baseline(n_envs_sample=4096, steps=200, seed=0):
     """Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of the same workload."""
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
@@ -69,7 +71,7 @@ def main():
     ap.add_argument("--envs-per-block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
-    ap.add_argument("--cpu-sample-steps", type=int, default=100)
+    ap.add_argument("--cpu-sample-steps", type=int, default=200)
     ap.add_argument("--no-gather", action="store_true")
     args = ap.parse_args()
 
@@ -101,9 +103,18 @@ def main():
         payload = torch.empty((n, 26), dtype=torch.float64, device=dev)
         glist = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
 
-    def one_step():
+    step_events = []
+
+    def one_step(timed=False):
         a = lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device=dev, generator=gen)
+        if timed:  # HIP events on the stream the library launches on (torch's current stream)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         obs, rew, term, trunc, _ = batch.step(a)
+        if timed:
+            e1.record()
+            step_events.append((e0, e1))
         if gather:
             payload[:, :24] = obs
             payload[:, 24] = rew
@@ -112,6 +123,7 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    ovf0 = batch.overflow_count()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -120,20 +132,18 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    kernel_ms = []
     for i in range(args.steps):
-        one_step()
-        if i == args.steps - 1 or (i % 10 == 0 and rank == 0 and i > 0):
-            pass
+        one_step(timed=True)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    # dominant kernel duration: HIP events recorded by the library around its last k_env_step launch
-    step_kernel_ms = batch.last_step_ms()
+    # dominant kernel: average over the timed region of the step launches (compact tier + fallback)
+    step_kernel_ms = sum(a.elapsed_time(b) for a, b in step_events) / len(step_events)
     ev_ms = ev0.elapsed_time(ev1)
+    fallback = batch.overflow_count() - ovf0
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -175,11 +185,16 @@ def main():
             "data": "synthetic (uniform random actions in the ur3e-v2 action Box; stochastic 'high' mug resets)",
             "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
-                       "envs_per_block": batch.cfg.envs_per_block if batch.cfg.envs_per_block else 16,
+                       "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (LDS working set, 4 envs/CU)"
+                                            " + full-capacity fallback", -128: "full-capacity, 128 lanes per env",
+                                            -64: "full-capacity, 64 lanes per env"}.get(
+                           batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
+            "fallback_env_steps_frac": fallback / float(n * args.steps),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic,
-                         "kernel": "k_env_step", "kernel_ms": step_kernel_ms,
+                         "kernel": "w_env_step<64,KSS_NV> (+ w_env_step_list<128> fallback)",
+                         "kernel_ms": step_kernel_ms,
                          "stream_avg_ms": kernel_avg_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
                          "note": "path is FP64-latency-bound (SURVEY.md §8d); HBM fraction reported as required"},

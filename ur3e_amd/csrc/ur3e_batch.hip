@@ -621,7 +621,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
 
 /* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
 template <int NT, class KS>
-WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, int e, KS& s, WOut& o) {
+WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
   const int tid = threadIdx.x;
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = c.reset_key >= 0 ? m->key_qpos[c.reset_key][k] : m->qpos0[k];
   for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = c.reset_key >= 0 ? m->key_qvel[c.reset_key][k] : 0.0; s.warm[k] = 0; }
@@ -643,11 +643,22 @@ WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, in
     o.episode = ep + 1;
   }
   SYNC();
-  w_forward<NT>(m, pl, s);
-  if (KS::BAIL && s.ovf) return;
+}
+
+template <int NT, class KS>
+WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c, KS& s, WOut& o) {
+  const int tid = threadIdx.x;
   if (tid == 0 && c.task == UR3E_TASK_GYM_V2) w_obs_v2(m, s, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
+}
+
+template <int NT, class KS>
+WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, int e, KS& s, WOut& o) {
+  w_reset_prep<NT>(m, c, e, s, o);
+  w_forward<NT>(m, pl, s);
+  if (KS::BAIL && s.ovf) return;
+  w_reset_finish<NT>(m, pl, c, s, o);
 }
 
 /* one env-step of env e into LDS (s, o); false: the compact tier overflowed */
@@ -694,45 +705,63 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     for (int k = 0; k < m->nu; k++) s.ctrl[k] = ctrl[k];
   }
   SYNC();
-  int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
-  for (int sstep = 0; sstep < fs; sstep++) {
-    w_step<NT>(m, pl, s);
+  const int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
+  int sub = 0, retried = 0, resetting = 0;
+  w_step_pre<NT>(m, s);
+  for (;;) {
+    w_forward<NT>(m, pl, s);
     if (KS::BAIL && s.ovf) return false;
-  }
-  w_make_carry<NT>(m, pl, s, o.carry);
-  SYNC();
-  if (c.task != UR3E_TASK_GYM_V2) {
-    if (tid == 0) { o.t += 1; o.ep_len += 1; }
+    if (resetting) {
+      w_reset_finish<NT>(m, pl, c, s, o);
+      return true;
+    }
+    if (!retried && w_step_badacc<NT>(m, s)) {
+      retried = 1;
+      continue;
+    }
+    w_step_euler<NT>(m, pl, s);
+    retried = 0;
+    if (++sub < fs) {
+      w_step_pre<NT>(m, s);
+      continue;
+    }
+    w_make_carry<NT>(m, pl, s, o.carry);
     SYNC();
+    if (c.task != UR3E_TASK_GYM_V2) {
+      if (tid == 0) { o.t += 1; o.ep_len += 1; }
+      SYNC();
+      return true;
+    }
+    if (tid == 0) {
+      int t = o.t + 1;
+      o.t = t;
+      w_obs_v2(m, s, o.obs);
+      double r = k_reward_v2(o.obs, o.a);
+      int term = w_termination_v2(m, s, o.obs);
+      int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
+      double dx = o.obs[3] - o.obs[6], dy = o.obs[4] - o.obs[7], dz = o.obs[5] - o.obs[8];
+      if (sqrt(dx * dx + dy * dy + dz * dz) < 0.05) {
+        term = 1;
+        r += 50.0;
+      }
+      o.ep_return += r;
+      o.ep_len += 1;
+      o.r = r;
+      o.term = term;
+      o.trunc = trunc;
+    }
+    SYNC();
+    if ((o.term || o.trunc) && c.auto_reset) {
+      for (int k = tid; k < 24; k += NT) o.tobs[k] = o.obs[k];
+      if (tid == 0) o.did_reset = 1;
+      SYNC();
+      w_reset_prep<NT>(m, c, e, s, o);
+      resetting = 1;
+      continue;
+    }
     return true;
   }
-  if (tid == 0) {
-    int t = o.t + 1;
-    o.t = t;
-    w_obs_v2(m, s, o.obs);
-    double r = k_reward_v2(o.obs, o.a);
-    int term = w_termination_v2(m, s, o.obs);
-    int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
-    double dx = o.obs[3] - o.obs[6], dy = o.obs[4] - o.obs[7], dz = o.obs[5] - o.obs[8];
-    if (sqrt(dx * dx + dy * dy + dz * dz) < 0.05) {
-      term = 1;
-      r += 50.0;
-    }
-    o.ep_return += r;
-    o.ep_len += 1;
-    o.r = r;
-    o.term = term;
-    o.trunc = trunc;
-  }
-  SYNC();
-  if ((o.term || o.trunc) && c.auto_reset) {
-    for (int k = tid; k < 24; k += NT) o.tobs[k] = o.obs[k];
-    if (tid == 0) o.did_reset = 1;
-    SYNC();
-    w_reset_env<NT>(m, pl, c, e, s, o);
-    if (KS::BAIL && s.ovf) return false;
-  }
-  return true;
 }
 
 template <int NT>

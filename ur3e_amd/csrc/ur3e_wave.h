@@ -1367,8 +1367,10 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   WT(15);
 }
 
+/* mj_step pieces around the forward pass, so a caller can keep ONE inlined copy of w_forward
+   (the kernel is large; a single copy keeps its instruction footprint down) */
 template <int NT, class KS>
-WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
+WD void w_step_pre(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nq = m->nq, nv = NVOF(KS, m);
   if (tid == 0) {
@@ -1384,8 +1386,13 @@ WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (tid == 0) s.nwarn++;
     SYNC();
   }
-  w_forward<NT>(m, pl, s);
-  if (KS::BAIL && s.ovf) return;
+}
+
+/* after the first forward of a substep: bad qacc -> reset state, returns 1 (forward again) */
+template <int NT, class KS>
+WD int w_step_badacc(KModel m, KS& s) {
+  const int tid = threadIdx.x;
+  const int nq = m->nq, nv = NVOF(KS, m);
   if (tid == 0) {
     int bad = 0;
     for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qacc[k]);
@@ -1397,9 +1404,15 @@ WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (tid < nv) { s.qvel[tid] = 0; s.warm[tid] = 0; }
     if (tid == 0) s.nwarn++;
     SYNC();
-    w_forward<NT>(m, pl, s);
-    if (KS::BAIL && s.ovf) return;
+    return 1;
   }
+  return 0;
+}
+
+template <int NT, class KS>
+WD void w_step_euler(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = NVOF(KS, m);
   /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
   int damped = 0;
   for (int k = 0; k < nv; k++) damped |= m->dof_damping[k] > 0;
@@ -1446,6 +1459,18 @@ WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if (tid < nv) s.warm[tid] = s.qacc[tid];
   SYNC();
   WT(17);
+}
+
+template <int NT, class KS>
+WD void w_step(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  w_step_pre<NT>(m, s);
+  w_forward<NT>(m, pl, s);
+  if (KS::BAIL && s.ovf) return;
+  if (w_step_badacc<NT>(m, s)) {
+    w_forward<NT>(m, pl, s);
+    if (KS::BAIL && s.ovf) return;
+  }
+  w_step_euler<NT>(m, pl, s);
 }
 
 #endif /* UR3E_WAVE_H */
