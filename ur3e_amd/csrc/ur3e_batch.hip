@@ -955,6 +955,18 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     if (m->dof_frictionloss[v] > 0) pl->floss_dof[pl->nfloss++] = v;
   for (int b = 0; b < m->nbody; b++)
     if (m->body_jntnum[b] > pl->max_jntnum) pl->max_jntnum = m->body_jntnum[b];
+  /* fixed row groups: equality constraints, then dof frictionloss (w_make_constraint's order) */
+  int ng = 0, nr = 0;
+  for (int e = 0; e < m->neq; e++) {
+    pl->fix_type[ng] = m->eq_type[e] == UR3E_EQ_CONNECT ? G_CONNECT : G_JOINTEQ;
+    pl->fix_id[ng] = e; pl->fix_row[ng] = nr; ng++;
+    nr += m->eq_type[e] == UR3E_EQ_CONNECT ? 3 : 1;
+  }
+  for (int k = 0; k < pl->nfloss; k++) {
+    pl->fix_type[ng] = G_FLOSS; pl->fix_id[ng] = pl->floss_dof[k]; pl->fix_row[ng] = nr; ng++; nr++;
+  }
+  pl->nfixgrp = ng;
+  pl->nfixrow = nr;
 }
 
 extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
@@ -1141,6 +1153,57 @@ extern "C" int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, 
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }
+
+#ifdef UR3E_STAGE_TIMING
+/* diagnostic: cycles of ONE stage of the compact tier, repeated `reps` times on each env's
+   primed LDS state (w_forward once first) */
+__global__ __launch_bounds__(64) void w_stage_bench(const ur3e_model_t* __restrict__ m,
+                                                    const KPlan* __restrict__ pl, KConfig c, KState st, int stage,
+                                                    int reps, unsigned long long* __restrict__ cyc) {
+  __shared__ KSS_NV s;
+  __shared__ WOut o;
+  const int e = blockIdx.x;
+  if (e >= st.n) return;
+  w_load<64>(m, c, st, e, s, o);
+  SYNC64();
+  w_forward<64>(m, pl, s);
+  if (s.ovf) { if (threadIdx.x == 0) cyc[e] = 0; return; }
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < reps; r++) {
+    switch (stage) {
+      case 0: r_kinematics(m, pl, s); break;
+      case 1: w_com_pos<64>(m, pl, s); break;
+      case 2: w_crb<64>(m, s); break;
+      case 3: w_collision<64>(m, s); break;
+      case 4: w_make_constraint<64>(m, pl, s); break;
+      case 5: r_vel_acc(m, pl, s); break;
+      case 6: w_rne_passive<64>(m, pl, s); break;
+      case 7: { double x = r_tree_solve(m, pl, s, false, threadIdx.x < 20 ? s.qfrc_smooth[threadIdx.x] : 0.0);
+                if (threadIdx.x < 20) s.qacc_smooth[threadIdx.x] = x; SYNC64(); } break;
+      case 8: r_solve_newton(m, s); break;
+      case 9: w_forward<64>(m, pl, s); break;
+      case 10: r_kinematics<KSS_NV, 1>(m, pl, s); break;
+      case 11: r_kinematics<KSS_NV, 2>(m, pl, s); break;
+      case 12: r_kinematics<KSS_NV, 3>(m, pl, s); break;
+      case 13: w_make_constraint<64, KSS_NV, 1>(m, pl, s); break;
+      case 14: w_make_constraint<64, KSS_NV, 2>(m, pl, s); break;
+      case 15: w_make_constraint<64, KSS_NV, 3>(m, pl, s); break;
+      default: break;
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[e] = (t1 - t0) / (unsigned long long)(reps > 0 ? reps : 1);
+}
+
+extern "C" int ur3e_debug_stage_bench(ur3e_batch_t* b, int stage, int reps, unsigned long long* d_cycles) {
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(w_stage_bench, dim3(b->n), dim3(64), 0, 0, b->d_model, b->d_plan, b->cfg, b->st, stage, reps,
+                     d_cycles);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return UR3E_OK;
+}
+#endif
 
 /* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */
 extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {

@@ -40,6 +40,9 @@ struct KPlan {
   int floss_dof[K_NV];
   int neq_rows;
   int max_jntnum; /* joints on the busiest body (the compact tier's body passes need <= 1) */
+  /* row groups that exist every step (equality, then frictionloss), in oracle order */
+  int nfixgrp, nfixrow;
+  int fix_type[UR3E_MAXEQ + K_NV], fix_id[UR3E_MAXEQ + K_NV], fix_row[UR3E_MAXEQ + K_NV];
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -132,6 +135,7 @@ __device__ __forceinline__ void wsync() {
   }
 }
 #define SYNC() wsync<NT>()
+#define SYNC64() wsync<64>()
 #define WD __device__ static __forceinline__
 
 /* diagnostic build only (-DUR3E_STAGE_TIMING): per-stage shader-clock cycles, lane 0 of every env */
@@ -535,10 +539,17 @@ KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double
   s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
 }
 
-template <int NT, class KS>
+template <int NT, class KS, int VAR = 0>
 WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nv = NVOF(KS, m);
+  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64);
+  if constexpr (REG) {
+    r_mc_layout(m, pl, s);
+    if (s.ovf) return;
+    if constexpr (VAR == 1) return;
+    r_mc_rows(m, pl, s);
+  } else {
   /* lane 0 lays out the row groups in oracle order; a group that does not fit stops the layout */
   if (tid == 0) {
     int nrow = 0, ng = 0, stop = 0;
@@ -575,6 +586,7 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   SYNC();
   if (KS::BAIL && s.ovf) return;
+  if constexpr (VAR == 1) return;
   /* phase A: Jacobian entries, one lane per (group, dof) */
   const int nitem = s.ngrp * nv;
   for (int it = tid; it < nitem; it += NT) {
@@ -643,7 +655,10 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   SYNC();
+  }
+  if constexpr (VAR == 2) return;
   /* phase B: reference acceleration and regulariser, one lane per row */
+  if constexpr (!REG)
   for (int r = tid; r < s.nefc; r += NT) {
     int g = s.efc_grp[r];
     int type = s.grp_type[g], id = s.grp_id[g];
@@ -694,6 +709,7 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   SYNC();
+  if constexpr (VAR == 3) return;
   /* phase C: elliptic regularisation per contact */
   for (int g = tid; g < s.ngrp; g += NT) {
     if (s.grp_type[g] != G_CONTACT) continue;

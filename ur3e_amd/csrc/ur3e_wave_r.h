@@ -180,11 +180,13 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
 #pragma unroll
   for (int i = 0; i < K_NV; i++)
     if (i < nv) a0 += rl(term, i);
-  for (int i = 0; i < nefc; i++) {
-    double f = rl(w.F, i);
-    double n = a1 + f;
+  /* rows >= nefc carry flag 0, so the capacity-bound loop needs no branch */
+#pragma unroll
+  for (int i = 0; i < KS::MAXEFC; i++) {
+    double n = a1 + rl(w.F, i);
     a1 = rli(w.flag, i) ? n : a1; /* select, not a skipped add: -0 stays -0 as in the oracle */
   }
+  (void)nefc;
   gauss = 0.5 * a0;
   cost = gauss + a1;
 }
@@ -196,7 +198,11 @@ WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double q
   const int nefc = s.nefc;
   const int col = lane < K_NV ? lane : 0;
   double f = 0;
-  for (int i = 0; i < nefc; i++) f += s.efc_J[i][col] * rl(w.force, i);
+#pragma unroll
+  for (int i = 0; i < KS::MAXEFC; i++) {
+    double n = f + s.efc_J[i][col] * rl(w.force, i);
+    f = i < nefc ? n : f;
+  }
   qfrc_c = f;
   grad = Ma - qs - f;
 }
@@ -240,51 +246,63 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   const int row = lane < nv ? lane : 0;
-  double h[K_NV];
+  /* H = M + J'DJ + cone blocks in ELEMENT layout: lane owns lower-triangle elements
+     e = lane + 64 q (q < 4), each accumulating rows in oracle order; then one LDS transpose
+     hands row k to lane k for the factorisation */
+  constexpr int NQ = (K_NV * (K_NV + 1) / 2 + 63) / 64;
+  const int nel = nv * (nv + 1) / 2;
+  int ek[NQ], ec[NQ];
+  bool ev[NQ];
+  double hv[NQ];
 #pragma unroll
-  for (int c = 0; c < K_NV; c++) h[c] = s.qM[row][c];
-  /* rows in oracle order; row i's broadcast J row is loaded one iteration ahead */
-  double jn[K_NV], jrn = 0;
-  if (nefc > 0) {
-#pragma unroll
-    for (int c = 0; c < K_NV; c++) jn[c] = s.efc_J[0][c];
-    jrn = s.efc_J[0][row];
+  for (int q = 0; q < NQ; q++) {
+    int e = lane + 64 * q;
+    ev[q] = e < nel;
+    int k = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    while (k * (k + 1) / 2 > e) k--;
+    while ((k + 1) * (k + 2) / 2 <= e) k++;
+    if (!ev[q]) k = 0;
+    ek[q] = k;
+    ec[q] = ev[q] ? e - k * (k + 1) / 2 : 0;
+    hv[q] = s.qM[ek[q]][ec[q]];
   }
   for (int i = 0; i < nefc; i++) {
-    double jc[K_NV];
-#pragma unroll
-    for (int c = 0; c < K_NV; c++) jc[c] = jn[c];
-    const double jr = jrn;
-    if (i + 1 < nefc) {
-#pragma unroll
-      for (int c = 0; c < K_NV; c++) jn[c] = s.efc_J[i + 1][c];
-      jrn = s.efc_J[i + 1][row];
-    }
     const int st = rli(w.st, i);
     if (st == ST_QUADRATIC) {
-      const double djr = rl(w.D, i) * jr;
-      const bool use = jr != 0;
+      const double D = rl(w.D, i);
 #pragma unroll
-      for (int c = 0; c < K_NV; c++) {
-        double n = h[c] + djr * jc[c];
-        h[c] = use ? n : h[c];
+      for (int q = 0; q < NQ; q++) {
+        const double jk = s.efc_J[i][ek[q]], jc = s.efc_J[i][ec[q]];
+        const double djr = D * jk;
+        const double n = hv[q] + djr * jc;
+        hv[q] = jk != 0 ? n : hv[q];
       }
     } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
       const double* Hc = s.con_Hc[s.efc_id[i]];
-      double t[3];
-      for (int j = 0; j < 3; j++) {
-        double acc = 0;
-        for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[i + k][row];
-        t[j] = acc;
-      }
 #pragma unroll
-      for (int c = 0; c < K_NV; c++) {
+      for (int q = 0; q < NQ; q++) {
+        double t[3];
+        for (int j = 0; j < 3; j++) {
+          double acc = 0;
+          for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[i + k][ek[q]];
+          t[j] = acc;
+        }
         double acc = 0;
-        for (int j = 0; j < 3; j++) acc += s.efc_J[i + j][c] * t[j];
-        h[c] += acc;
+        for (int j = 0; j < 3; j++) acc += s.efc_J[i + j][ec[q]] * t[j];
+        hv[q] += acc;
       }
     }
   }
+#pragma unroll
+  for (int q = 0; q < NQ; q++)
+    if (ev[q]) s.H[ek[q]][ec[q]] = hv[q];
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  double h[K_NV];
+#pragma unroll
+  for (int c = 0; c < K_NV; c++) h[c] = c <= row ? s.H[row][c] : 0.0;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
   WT(10);
   /* right-looking Cholesky, lane = row; element (i,k) gets -= L[i][j] L[k][j] for j = 0,1,...
      (the oracle's left-looking order) */
@@ -344,6 +362,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 }
 
 /* line-search 1-D evaluation at a (w_ls_eval): per-row terms on the row lanes, ordered sums */
+template <int ME>
 WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF, double& lsdF,
                   double& lsd2F) {
   const int lane = threadIdx.x;
@@ -450,7 +469,7 @@ WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma
   }
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
-  r_ls_eval(w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
+  r_ls_eval<KS::MAXEFC>(w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
   if (d0 >= 0) return 0;
   double lo = 0.0, dlo = d0, hlo = h0;
   double hi = -1.0, dhi = 0, hhi = 0;
@@ -458,7 +477,7 @@ WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma
   double a = -d0 / h0;
   for (int it = 0; it < m->ls_iterations; it++) {
     double f, df, d2f;
-    r_ls_eval(w, nefc, a, gauss, g1, g2, f, df, d2f);
+    r_ls_eval<KS::MAXEFC>(w, nefc, a, gauss, g1, g2, f, df, d2f);
     if (f < bestF) { bestF = f; bestA = a; }
     if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
     if (df < 0) { lo = a; dlo = df; hlo = d2f; }
@@ -627,8 +646,8 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
    costs one LDS read of the parent + the arithmetic, not a chain of dependent global loads;
    bodies carry at most one joint (KPlan.max_jntnum <= 1, checked by the caller) */
 
-/* w_kinematics (mj_kinematics) */
-template <class KS>
+/* w_kinematics (mj_kinematics); VAR != 0 only in the diagnostic stage bench */
+template <class KS, int VAR = 0>
 WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = threadIdx.x;
   const int nb = m->nbody, nlevel = pl->nlevel;
@@ -661,6 +680,10 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   /* hinge rotation of this body's joint (w_kinematics' qloc pass) */
   double ql[4] = {1, 0, 0, 0};
   if (depth > 0 && jn == 1 && jt != UR3E_JNT_FREE) k_axis_angle_quat(ql, jax, s.qpos[qa] - q0);
+  if constexpr (VAR == 1) {
+    if (lane < 64) s.xpos[lane % 25][0] = ql[0] + bpos[0] + jax[0] + jps[0] + bquat[0] + fpos[0] + fquat[0] + fb;
+    return;
+  }
   if (lane == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
@@ -669,7 +692,11 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   for (int lvl = 1; lvl <= nlevel; lvl++) {
-    if (depth == lvl) {
+    if (VAR == 2 && depth == lvl) {
+      for (int c = 0; c < 9; c++) s.xmat[lane][c] = s.xmat[pid][c] + bpos[0];
+      for (int c = 0; c < 3; c++) s.xpos[lane][c] = s.xpos[pid][c] + jps[0];
+      for (int c = 0; c < 4; c++) s.xquat[lane][c] = s.xquat[pid][c] + ql[0];
+    } else if (depth == lvl) {
       double xpos[3], xquat[4];
       if (jn == 1 && jt == UR3E_JNT_FREE) {
         xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
@@ -707,6 +734,7 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+  if constexpr (VAR == 3) return;
   if (lane < nfr) {
     double bp[3], bq[4], bm[9], op[3], om[9];
     for (int c = 0; c < 3; c++) bp[c] = s.xpos[fb][c];
@@ -837,6 +865,271 @@ WD void r_cfrc(KModel m, KS& s) {
   }
   if (lane < nb) {
     for (int r = 0; r < 6; r++) cfrc[lane][r] = lane == 0 ? 0.0 : f[r];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+/* ================================================================== */
+/* constraint rows for the compact tier: layout and Jacobian            */
+/* ================================================================== */
+/* Row-group layout in the oracle's order (equality, frictionloss: host-precomputed in KPlan;
+   joint limits in (joint, side) order; condim-3 contacts in contact order) by ballot prefix
+   sums instead of a serial lane-0 walk.  Any layout that would not fit the compact capacity
+   bails (ovf): the full-capacity tier then reproduces the oracle's truncation rule. */
+template <class KS>
+WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int lane = threadIdx.x;
+  const int nj = m->njnt, ncon = s.ncon;
+  int lo = 0, hi = 0;
+  if (lane < nj && m->jnt_limited[lane] &&
+      (m->jnt_type[lane] == UR3E_JNT_HINGE || m->jnt_type[lane] == UR3E_JNT_SLIDE)) {
+    const double q = s.qpos[m->jnt_qposadr[lane]];
+    const double mg = m->jnt_margin[lane];
+    const double dlo = -1.0 * (m->jnt_range[lane][0] - q);
+    const double dhi = 1.0 * (m->jnt_range[lane][1] - q);
+    lo = dlo < mg;
+    hi = dhi < mg;
+  }
+  int c3 = 0;
+  if (lane < ncon) c3 = m->cpair_condim[s.con_cpair[lane]] == 3;
+  const unsigned long long mlo = __ballot(lo), mhi = __ballot(hi), mc = __ballot(c3);
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int nfix = pl->nfixgrp, nfixrow = pl->nfixrow;
+  const int nlim = __popcll(mlo) + __popcll(mhi);
+  const int ncg = __popcll(mc);
+  const int nrow = nfixrow + nlim + 3 * ncg;
+  const int ngrp = nfix + nlim + ncg;
+  if (nrow > KS::MAXEFC) {
+    if (lane == 0) s.ovf = 1;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    return;
+  }
+  /* group g's rows get type/id/group (+ frictionloss, contact back-pointer) */
+  auto put = [&](int g, int type, int id, int r) {
+    s.grp_type[g] = type; s.grp_id[g] = id; s.grp_row[g] = r;
+    const int n = (type == G_CONNECT || type == G_CONTACT) ? 3 : 1;
+    const int ct = type == G_CONNECT || type == G_JOINTEQ ? CN_EQUALITY
+                 : type == G_FLOSS ? CN_FRICTION_DOF : type == G_LIMIT ? CN_LIMIT_JOINT : CN_CONTACT_ELLIPTIC;
+    const int cid = type == G_LIMIT ? (id >> 1) : id;
+    const double fl = type == G_FLOSS ? m->dof_frictionloss[id] : 0.0;
+    for (int k = 0; k < n; k++) {
+      s.efc_type[r + k] = ct; s.efc_id[r + k] = cid; s.efc_grp[r + k] = g; s.efc_floss[r + k] = fl;
+    }
+    if (type == G_CONTACT) s.con_efc[id] = r;
+  };
+  if (lane < nfix) put(lane, pl->fix_type[lane], pl->fix_id[lane], pl->fix_row[lane]);
+  const int loff = __popcll(mlo & below) + __popcll(mhi & below);
+  if (lo) put(nfix + loff, G_LIMIT, 2 * lane, nfixrow + loff);
+  if (hi) put(nfix + loff + lo, G_LIMIT, 2 * lane + 1, nfixrow + loff + lo);
+  if (c3) {
+    const int k = __popcll(mc & below);
+    put(nfix + nlim + k, G_CONTACT, lane, nfixrow + nlim + 3 * k);
+  }
+  if (lane == 0) { s.ngrp = ngrp; s.nefc = nrow; }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+/* Jacobian rows and per-row impedance for the compact tier.
+   1. lane = group: the group's geometry (offsets to subtree coms, contact frame, dof masks) and
+      its rows' impedance inputs (pos, margin, diag, solref/solimp) into registers;
+   2. lane = dof: walk the groups in order, each group's data broadcast by readlane, one code
+      path per group type (uniform) -> J columns;
+   3. lane = row: fetch its group's inputs by lane shuffle, then one common impedance path.
+   Same expressions as w_make_constraint's phases A and B. */
+template <class KS>
+WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int lane = threadIdx.x;
+  const int nv = NVOF(KS, m);
+  const int ngrp = s.ngrp, nefc = s.nefc;
+  /* ---- 1. per-group data (lane = group) ---- */
+  int gtype = -1, grow = 0, msk1 = 0, msk2 = 0, dof1 = -1, dof2 = -1, fric = 0;
+  double o1[3] = {0, 0, 0}, o2[3] = {0, 0, 0}, fr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double gpos[3] = {0, 0, 0}, gmargin = 0, gdiag = 0, dpoly = 0, side = 0;
+  double sref[2] = {0, 0}, simp[5] = {0, 0, 0, 0, 0};
+  if (lane < ngrp) {
+    gtype = s.grp_type[lane];
+    const int id = s.grp_id[lane];
+    grow = s.grp_row[lane];
+    if (gtype == G_CONNECT) {
+      const int e = id;
+      const int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      double xm1[9], xm2[9], ed1[3], ed2[3];
+      for (int k = 0; k < 9; k++) { xm1[k] = s.xmat[b1][k]; xm2[k] = s.xmat[b2][k]; }
+      for (int k = 0; k < 3; k++) { ed1[k] = m->eq_data[e][k]; ed2[k] = m->eq_data[e][3 + k]; }
+      double p1[3], p2[3];
+      k_mat_vec3(p1, xm1, ed1);
+      p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
+      k_mat_vec3(p2, xm2, ed2);
+      p2[0] += s.xpos[b2][0]; p2[1] += s.xpos[b2][1]; p2[2] += s.xpos[b2][2];
+      const int r1 = m->body_rootid[b1], r2 = m->body_rootid[b2];
+      for (int k = 0; k < 3; k++) {
+        o1[k] = p1[k] - s.subtree_com[r1][k];
+        o2[k] = p2[k] - s.subtree_com[r2][k];
+        gpos[k] = p1[k] - p2[k];
+      }
+      msk1 = pl->body_dof_mask[b1]; msk2 = pl->body_dof_mask[b2];
+      gdiag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      for (int k = 0; k < 2; k++) sref[k] = m->eq_solref[e][k];
+      for (int k = 0; k < 5; k++) simp[k] = m->eq_solimp[e][k];
+    } else if (gtype == G_JOINTEQ) {
+      const int e = id;
+      const int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
+      const double* c = m->eq_data[e];
+      dof1 = m->jnt_dofadr[j1];
+      const int a1 = m->jnt_qposadr[j1];
+      const double q1 = s.qpos[a1] - m->qpos0[a1];
+      gdiag = m->dof_invweight0[dof1];
+      if (j2 >= 0) {
+        dof2 = m->jnt_dofadr[j2];
+        const int a2 = m->jnt_qposadr[j2];
+        const double q2 = s.qpos[a2] - m->qpos0[a2];
+        dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
+        gpos[0] = q1 - (c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4]))));
+        gdiag += m->dof_invweight0[dof2];
+      } else {
+        gpos[0] = q1 - c[0];
+      }
+      for (int k = 0; k < 2; k++) sref[k] = m->eq_solref[e][k];
+      for (int k = 0; k < 5; k++) simp[k] = m->eq_solimp[e][k];
+    } else if (gtype == G_FLOSS) {
+      dof1 = id;
+      gdiag = m->dof_invweight0[id];
+      fric = 1;
+      for (int k = 0; k < 2; k++) sref[k] = m->dof_solref[id][k];
+      for (int k = 0; k < 5; k++) simp[k] = m->dof_solimp[id][k];
+    } else if (gtype == G_LIMIT) {
+      const int j = id >> 1;
+      const int sd = (id & 1) ? 1 : -1;
+      side = (double)sd;
+      dof1 = m->jnt_dofadr[j];
+      const double q = s.qpos[m->jnt_qposadr[j]];
+      gpos[0] = sd * (m->jnt_range[j][(sd + 1) / 2] - q);
+      gmargin = m->jnt_margin[j];
+      gdiag = m->dof_invweight0[dof1];
+      for (int k = 0; k < 2; k++) sref[k] = m->jnt_solref[j][k];
+      for (int k = 0; k < 5; k++) simp[k] = m->jnt_solimp[j][k];
+    } else {
+      const int c = id;
+      const int p = s.con_cpair[c];
+      const int b1 = m->geom_bodyid[s.con_geom1[c]], b2 = m->geom_bodyid[s.con_geom2[c]];
+      const int r1 = m->body_rootid[b1], r2 = m->body_rootid[b2];
+      for (int k = 0; k < 3; k++) {
+        const double pk = s.con_pos[c][k];
+        o1[k] = pk - s.subtree_com[r1][k];
+        o2[k] = pk - s.subtree_com[r2][k];
+      }
+      for (int k = 0; k < 9; k++) fr[k] = s.con_frame[c][k];
+      msk1 = pl->body_dof_mask[b1]; msk2 = pl->body_dof_mask[b2];
+      const double d = s.con_dist[c];
+      gpos[0] = d; gpos[1] = d; gpos[2] = d;
+      gmargin = m->cpair_margin[p] - m->cpair_gap[p];
+      gdiag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+      fric = 2; /* rows k > 0 */
+      for (int k = 0; k < 2; k++) sref[k] = m->cpair_solref[p][k];
+      for (int k = 0; k < 5; k++) simp[k] = m->cpair_solimp[p][k];
+    }
+  }
+  /* ---- 2. Jacobian, lane = dof, groups in order ---- */
+  {
+    const int v = lane < nv ? lane : 0;
+    double cd[6];
+    for (int r = 0; r < 6; r++) cd[r] = s.cdof[v][r];
+    const unsigned int vbit = 1u << v;
+    for (int g = 0; g < ngrp; g++) {
+      const int type = rli(gtype, g), r = rli(grow, g);
+      if (type == G_CONNECT || type >= G_CONTACT) {
+        const unsigned int m1 = (unsigned int)rli(msk1, g), m2 = (unsigned int)rli(msk2, g);
+        double a1[3], a2[3], j1[3], j2[3];
+        for (int k = 0; k < 3; k++) { a1[k] = rl(o1[k], g); a2[k] = rl(o2[k], g); }
+        if (m1 & vbit) {
+          double cr[3];
+          k_cross3(cr, cd, a1);
+          j1[0] = cd[3] + cr[0]; j1[1] = cd[4] + cr[1]; j1[2] = cd[5] + cr[2];
+        } else {
+          j1[0] = 0; j1[1] = 0; j1[2] = 0;
+        }
+        if (m2 & vbit) {
+          double cr[3];
+          k_cross3(cr, cd, a2);
+          j2[0] = cd[3] + cr[0]; j2[1] = cd[4] + cr[1]; j2[2] = cd[5] + cr[2];
+        } else {
+          j2[0] = 0; j2[1] = 0; j2[2] = 0;
+        }
+        if (type == G_CONNECT) {
+          if (lane < nv)
+            for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = j1[k] - j2[k];
+        } else {
+          double f[9];
+          for (int k = 0; k < 9; k++) f[k] = rl(fr[k], g);
+          const double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
+          if (lane < nv)
+            for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = f[3 * k] * dj0 + f[3 * k + 1] * dj1 + f[3 * k + 2] * dj2;
+        }
+      } else if (type == G_JOINTEQ) {
+        const int d1 = rli(dof1, g), d2 = rli(dof2, g);
+        const double dp = rl(dpoly, g);
+        double val = 0;
+        if (v == d1) val = 1;
+        if (d2 >= 0 && v == d2) val = -dp;
+        if (lane < nv) s.efc_J[r][v] = val;
+      } else if (type == G_FLOSS) {
+        const int d1 = rli(dof1, g);
+        if (lane < nv) s.efc_J[r][v] = v == d1 ? 1.0 : 0.0;
+      } else {
+        const int d1 = rli(dof1, g);
+        const double sd = rl(side, g);
+        if (lane < nv) s.efc_J[r][v] = v == d1 ? -sd : 0.0;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  /* ---- 3. impedance, lane = row (w_row_impedance) ---- */
+  {
+    const int r = lane;
+    const int g = lane < nefc ? s.efc_grp[r] : 0;
+    const int k = lane < nefc ? r - s.grp_row[g] : 0;
+    const double p0 = shf(gpos[0], g), p1 = shf(gpos[1], g), p2 = shf(gpos[2], g);
+    const double pos = k == 0 ? p0 : (k == 1 ? p1 : p2);
+    const double margin = shf(gmargin, g), diag = shf(gdiag, g);
+    const int fr_ = shfi(fric, g);
+    const int friction_row = fr_ == 1 || (fr_ == 2 && k > 0);
+    double sr[2], si[5];
+    for (int q = 0; q < 2; q++) sr[q] = shf(sref[q], g);
+    for (int q = 0; q < 5; q++) si[q] = shf(simp[q], g);
+    if (lane < nefc) {
+      double jr[K_NV], qv[K_NV];
+#pragma unroll
+      for (int q = 0; q < K_NV; q++) { jr[q] = s.efc_J[r][q]; qv[q] = s.qvel[q]; }
+      double vel = 0;
+#pragma unroll
+      for (int q = 0; q < K_NV; q++)
+        if (q < nv) vel += jr[q] * qv[q];
+      double imp = k_get_impedance(si, pos, margin);
+      double dmax = si[1];
+      if (dmax < K_MINIMP) dmax = K_MINIMP;
+      if (dmax > K_MAXIMP) dmax = K_MAXIMP;
+      double K, B;
+      if (sr[0] > 0) {
+        double tc = sr[0];
+        if (tc < 2 * m->timestep) tc = 2 * m->timestep;
+        double dr = sr[1];
+        K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+        B = 2.0 / (dmax * tc);
+      } else {
+        K = -sr[0] / (dmax * dmax);
+        B = -sr[1] / dmax;
+      }
+      if (friction_row)
+        s.efc_aref[r] = -B * vel;
+      else
+        s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
+      double R = (1 - imp) * diag / imp;
+      s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
+    }
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
