@@ -1188,6 +1188,7 @@ __global__ __launch_bounds__(64) void w_stage_bench(const ur3e_model_t* __restri
       case 13: w_make_constraint<64, KSS_NV, 1>(m, pl, s); break;
       case 14: w_make_constraint<64, KSS_NV, 2>(m, pl, s); break;
       case 15: w_make_constraint<64, KSS_NV, 3>(m, pl, s); break;
+      case 16: w_collision<64, KSS_NV, 1>(m, s); break;
       default: break;
     }
   }

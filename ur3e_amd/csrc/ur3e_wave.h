@@ -453,7 +453,7 @@ WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
   return 0;
 }
 
-template <int NT, class KS>
+template <int NT, class KS, int VAR = 0>
 WD void w_collision(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int np = m->ncpair;
@@ -471,6 +471,7 @@ WD void w_collision(KModel m, KS& s) {
   }
   SYNC();
   if (KS::BAIL && s.ovf) return;
+  if constexpr (VAR == 1) return;
   for (int p = tid; p < np; p += NT) {
     int cnt = s.cand_count[p];
     int off = s.cand_off[p];

@@ -266,16 +266,31 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
     ec[q] = ev[q] ? e - k * (k + 1) / 2 : 0;
     hv[q] = s.qM[ek[q]][ec[q]];
   }
+  /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
+     compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
+     trips per element) */
+  double njk[NQ], njc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[0][ek[q]]; njc[q] = s.efc_J[0][ec[q]]; }
   for (int i = 0; i < nefc; i++) {
+    double jk[NQ], jc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      jk[q] = njk[q]; jc[q] = njc[q];
+      asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
+    }
+    const int inext = i + 1 < KS::MAXEFC ? i + 1 : i;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[inext][ek[q]]; njc[q] = s.efc_J[inext][ec[q]]; }
     const int st = rli(w.st, i);
     if (st == ST_QUADRATIC) {
       const double D = rl(w.D, i);
 #pragma unroll
       for (int q = 0; q < NQ; q++) {
-        const double jk = s.efc_J[i][ek[q]], jc = s.efc_J[i][ec[q]];
-        const double djr = D * jk;
-        const double n = hv[q] + djr * jc;
-        hv[q] = jk != 0 ? n : hv[q];
+        const double djr = D * jk[q];
+        double n = hv[q] + djr * jc[q];
+        asm volatile("" : "+v"(n));
+        hv[q] = jk[q] != 0 ? n : hv[q];
       }
     } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
       const double* Hc = s.con_Hc[s.efc_id[i]];
