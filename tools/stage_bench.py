@@ -19,7 +19,7 @@ for i in range(20):
 torch.cuda.synchronize()
 names = ["kinematics", "com_pos", "crb", "collision", "make_constraint", "vel_acc", "rne_passive",
          "tree_solve", "solve_newton", "forward(all)", "kin: preload only", "kin: levels copy-only",
-         "kin: no frames", "mc: layout only", "mc: +phase A (J)", "mc: +phase B (aref,R)"]
+         "kin: no frames", "mc: layout only", "mc: +phase A (J)", "mc: +phase B (aref,R)", "coll: count pass"]
 only = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else None
 cyc = torch.zeros(n, dtype=torch.int64, device="cuda")
 L.ur3e_debug_stage_bench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]

@@ -14,7 +14,7 @@ from ur3e_amd import runtime as rt
 names = {0: "kinematics", 1: "com_pos", 2: "crb+copy", 3: "factor_tree(M)", 4: "collision", 5: "make_constraint",
          6: "com_vel", 7: "rne+passive+act", 8: "solve_tree(smooth)", 9: "newton init (eval x2-3, grad)",
          10: "H build", 11: "cholesky / (r) backward solve", 12: "hessian_solve / (r) cholesky",
-         18: "(r) forward solve", 13: "line_search", 14: "eval+grad (iter)",
+         18: "(r) forward solve", 19: "(r) ls setup + eval(0)", 20: "(r) ls eval (per call)", 13: "line_search tail", 14: "eval+grad (iter)",
          15: "newton tail", 16: "euler factor+solve", 17: "integrate"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0

@@ -180,13 +180,10 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
 #pragma unroll
   for (int i = 0; i < K_NV; i++)
     if (i < nv) a0 += rl(term, i);
-  /* rows >= nefc carry flag 0, so the capacity-bound loop needs no branch */
-#pragma unroll
-  for (int i = 0; i < KS::MAXEFC; i++) {
-    double n = a1 + rl(w.F, i);
-    a1 = rli(w.flag, i) ? n : a1; /* select, not a skipped add: -0 stays -0 as in the oracle */
-  }
-  (void)nefc;
+  /* skipped rows contribute -0.0: x + (-0.0) == x exactly for every x (incl. -0, inf, NaN), so
+     the ordered sum needs neither a branch nor a select per row */
+  const double Fm0 = w.flag ? w.F : -0.0;
+  for (int i = 0; i < nefc; i++) a1 += rl(Fm0, i);
   gauss = 0.5 * a0;
   cost = gauss + a1;
 }
@@ -433,19 +430,19 @@ WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, do
   double aF = gauss + a * g1 + 0.5 * a * a * g2;
   double adF = g1 + a * g2;
   double ad2F = g2;
+  /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
+  const double Fm = flag ? F : -0.0, dFm = flag ? dF : -0.0, d2Fm = flag == 1 ? d2F : -0.0;
   for (int i = 0; i < nefc; i++) {
-    const int f = rli(flag, i);
-    double nF = aF + rl(F, i), ndF = adF + rl(dF, i), nd2F = ad2F + rl(d2F, i);
-    aF = f ? nF : aF;
-    adF = f ? ndF : adF;
-    ad2F = f == 1 ? nd2F : ad2F;
+    aF += rl(Fm, i);
+    adF += rl(dFm, i);
+    ad2F += rl(d2Fm, i);
   }
   lsF = aF; lsdF = adF; lsd2F = ad2F;
 }
 
 /* w_line_search: returns alpha (uniform); Jv on the row lanes */
 template <class KS>
-WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma, double qs, double gauss,
+WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, double qs, double gauss,
                         double scale) {
   const int lane = threadIdx.x;
   const int nv = NVOF(KS, m), nefc = s.nefc;
@@ -490,9 +487,11 @@ WD double r_line_search(KModel m, const KS& s, RRow& w, double search, double Ma
   double hi = -1.0, dhi = 0, hhi = 0;
   double bestA = 0.0, bestF = f0;
   double a = -d0 / h0;
+  WT(19);
   for (int it = 0; it < m->ls_iterations; it++) {
     double f, df, d2f;
     r_ls_eval<KS::MAXEFC>(w, nefc, a, gauss, g1, g2, f, df, d2f);
+    WT(20);
     if (f < bestF) { bestF = f; bestA = a; }
     if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
     if (df < 0) { lo = a; dlo = df; hlo = d2f; }
