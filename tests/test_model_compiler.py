@@ -74,3 +74,23 @@ def test_rest_contacts(main_model):
     assert f["ncon"] == 4
     f = po.forward_state(mc, np.array(md["key_qpos"][md["id_key_home"]]))
     assert f["ncon"] == 4
+
+
+def test_generated_main_tree_matches_model():
+    """csrc/gen_main_tree.h (compile-time dof tree of the specialised compact kernel) must equal
+    the ancestor masks of the shipped main.xml model image."""
+    import re
+    from ur3e_amd import _build
+    path = _build.gen_main_tree()
+    txt = open(path).read()
+    masks = [int(x, 16) for x in re.findall(r"0x([0-9a-f]+)u", txt)]
+    md = load_json(os.path.join(ASSETS, "main.model.json"))
+    par = md["dof_parentid"][:md["nv"]]
+    want = []
+    for i in range(md["nv"]):
+        m, j = 0, par[i]
+        while j >= 0:
+            m |= 1 << j
+            j = par[j]
+        want.append(m)
+    assert masks == want

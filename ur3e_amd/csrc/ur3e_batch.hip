@@ -888,6 +888,7 @@ struct ur3e_batch {
   int n;
   int wave_nt; /* 0: lane-per-env kernels (v1); 64/128: workgroup-per-env kernels (v2) */
   int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
+  int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
   int* d_ovf_list;
   int* d_ovf_count;
   unsigned long long* d_ovf_total;
@@ -1008,6 +1009,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.tier_con_cap = cfg->tier_con_cap;
   KPlan plan;
   build_plan(model, &plan);
+  b->main_tree = model->nv == UR3E_MAIN_NV;
+  for (int i = 0; i < model->nv && b->main_tree; i++)
+    if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) b->main_tree = 0;
   for (int k = 0; k < 12; k++) { c.gains.task[k] = cfg->task_gains[k]; c.gains.joint[k] = cfg->joint_gains[k]; }
   KState& s = b->st;
   s.n = n_envs;
@@ -1089,7 +1093,7 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
     HIPCHK(hipMemsetAsync(b->d_ovf_count, 0, sizeof(int), st));
-    if (b->host_model.nv == K_NV) /* main.xml: dof loops specialised at compile time */
+    if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
                          b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_count);

@@ -24,6 +24,7 @@
 #define UR3E_WAVE_H
 
 #include "ur3e_engine.h"
+#include "gen_main_tree.h"
 
 #define W_MAXCAND 128 /* collision candidates handled per env (main.xml: 92) */
 #define W_MAXGRP 96   /* constraint row groups */
@@ -52,9 +53,10 @@ struct KPlan {
 #define G_LIMIT 3
 #define G_CONTACT 4
 
-template <int MC, int ME, int NVC = 0>
+template <int MC, int ME, int NVC = 0, int TREE = 0>
 struct KSX {
   static constexpr int NV = NVC;    /* > 0: kernel specialised for a model with exactly NVC dofs */
+  static constexpr int STATIC_TREE = TREE; /* 1: main.xml's dof tree as compile-time tables */
   static constexpr int MAXCON = MC; /* contacts this tier holds */
   static constexpr int MAXEFC = ME; /* constraint rows this tier holds */
   static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
@@ -117,8 +119,10 @@ typedef KSX<K_MAXCON, K_MAXEFC> KSL;
 #define W_SMALL_MAXEFC 44
 #endif
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
-/* compact tier specialised for nv == K_NV (main.xml): every dof loop has a compile-time trip count */
-typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, K_NV> KSS_NV;
+/* compact tier specialised for main.xml: compile-time dof count and dof tree (gen_main_tree.h),
+   so dof loops have constant trip counts and tree tests fold away */
+typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1> KSS_NV;
+static_assert(UR3E_MAIN_NV <= K_NV, "main.xml dofs exceed K_NV");
 #define NVOF(KS, m) ((KS::NV) ? (KS::NV) : (m)->nv)
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the

@@ -581,7 +581,8 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   /* plan masks and damping up front: one batch of scalar loads, not one wait per column */
   unsigned int amask[K_NV];
 #pragma unroll
-  for (int k = 0; k < K_NV; k++) amask[k] = pl->dof_anc_mask[k];
+  for (int k = 0; k < K_NV; k++)
+    amask[k] = KS::STATIC_TREE ? (k < UR3E_MAIN_NV ? ur3e_main_dof_anc_mask[k] : 0u) : pl->dof_anc_mask[k];
   double a[K_NV];
 #pragma unroll
   for (int i = 0; i < K_NV; i++) a[i] = s.qM[i][col];
