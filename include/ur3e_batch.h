@@ -59,7 +59,8 @@ typedef struct ur3e_config_t {
   int frame_skip;        /* physics substeps per env-step (gym ur3e-v2: 2) */
   int max_episode_steps; /* truncation horizon (ur3e-v2: 2500); <= 0: never */
   int auto_reset;        /* SB3 VecEnv semantics on terminated|truncated */
-  int reset_noise;       /* 1: gym_utils.get_mug_xpos_noise("high") on reset */
+  int reset_noise;       /* mug xy noise on reset, gym_utils.get_mug_xpos_noise: 0 none ("deterministic"),
+                            1 "high" (ur3e-v2), 2 "med", 3 "low" */
   int reset_key;         /* keyframe index used by reset (-1: qpos0) */
   double task_gains[12]; /* kp_pos[3], kd_pos[3], kp_rot[3], kd_rot[3] (config_l_mug.yml) */
   double joint_gains[12];/* kp[6], kd[6] (config_j.yml) */
@@ -92,7 +93,9 @@ int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* d_obs, void
 
 /* one env-step for all envs.  d_actions [N, adim] row-major.  Outputs may be NULL:
    d_obs [N,24], d_reward [N], d_terminated/d_truncated [N] u8, d_terminal_obs [N,24]
-   (rows written only for envs that finished this step; d_obs then holds the reset obs). */
+   (rows written only for envs that finished this step; d_obs then holds the reset obs).
+   For the scripted tasks (TRAJ_L / MOVE_J / CTRL) d_obs, when given and the model has the
+   tcp / handle_site / ghost frames, receives the same 24-d observation of the new state. */
 int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adim, double* d_obs, double* d_reward,
                     uint8_t* d_terminated, uint8_t* d_truncated, double* d_terminal_obs, void* stream);
 
@@ -105,6 +108,16 @@ int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const double* d_
    d_nwarn [N] bad-value auto-resets (each may be NULL) */
 int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, double* d_ep_return, int* d_nwarn,
                         void* stream);
+
+/* stale-kinematics snapshot of the last forward, d_carry [N, 54]: tcp site_xpos (3), site_xmat (9),
+   the arm columns of mj_jacSite(tcp) as [jacp; jacr] 6x6 row-major (36), qfrc_bias[0:6] (6) --
+   what controller_func.py:68-117 reads from MjData before each pid_task_ctrl call */
+int ur3e_batch_get_carry(ur3e_batch_t* b, double* d_carry, void* stream);
+
+/* touch sensors of the last forward (main.xml: left/right pad sites, mjSENS_TOUCH semantics),
+   d_touch [N, ntouch]; replaces d.sensordata reads in controller/move_l_mug.py:79 via
+   utils/utils.py:238-240 (get_boolean_grasp_contact) */
+int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream);
 
 /* envs the compact tier handed to the full-capacity tier since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);

@@ -35,6 +35,11 @@ typedef struct {
   int tier_con_cap;
 } ur3o_config;
 
+/* the model has the sites the 24-d observation reads (main.xml) */
+static int has_obs_sites(const ur3e_model_t* m) {
+  return m->id_site_tcp >= 0 && m->id_site_handle >= 0 && m->id_body_ghost >= 0;
+}
+
 static void gains_from_cfg(const ur3o_config* c, ur3o_task_gains* tg, ur3o_joint_gains* jg) {
   for (int k = 0; k < 3; k++) {
     tg->kp_pos[k] = c->task_gains[k];
@@ -60,15 +65,19 @@ static void env_reset(const ur3e_model_t* m, const ur3o_config* c, ur3o_env* e, 
   if (c->reset_noise && m->id_body_fish >= 0) {
     double u0 = ur3o_uniform01(e->seed, e->env_id, e->episode, 0);
     double u1 = ur3o_uniform01(e->seed, e->env_id, e->episode, 1);
+    /* gym_utils.get_mug_xpos_noise: 1 "high", 2 "med", 3 "low" */
+    double ylo = -0.25, yhi = 0.2;
+    if (c->reset_noise == 2) { ylo = -0.2; yhi = 0.1; }
+    else if (c->reset_noise == 3) { ylo = -0.1; yhi = 0.01; }
     d->qpos[14] += 0.0 + (0.02 - 0.0) * u0;
-    d->qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+    d->qpos[15] += ylo + (yhi - ylo) * u1;
   }
   ur3o_forward(m, d);
   e->t = 0;
   e->ep_return = 0;
   e->ep_len = 0;
   e->episode++;
-  if (obs && c->task == 0) ur3o_obs_v2(m, d, obs);
+  if (obs && (c->task == 0 || has_obs_sites(m))) ur3o_obs_v2(m, d, obs);
 }
 
 /* envs: array of n ur3o_env (opaque to python: allocate n*ur3o_sizeof_env()) */
@@ -125,6 +134,8 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
     int fs = c->task == 3 ? c->frame_skip : 1;
     for (int s = 0; s < fs; s++) ur3o_step(m, d);
     e->t += 1;
+    /* task-space observation for the scripted tasks (same 24-d layout as ur3e-v2) */
+    if (obs && has_obs_sites(m)) ur3o_obs_v2(m, d, obs + 24 * (size_t)i);
   }
 }
 

@@ -45,6 +45,7 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
         np.testing.assert_array_equal(gobs, ob.obs)
     rng = np.random.default_rng(seed)
     max_dq = 0.0
+    max_touch = [0.0]
     for s in range(steps):
         a = action_fn(rng, n, md)
         o_obs, o_rew, o_term, o_trunc, o_tobs = ob.step(a)
@@ -64,8 +65,14 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
             np.testing.assert_array_equal(wa.cpu().numpy(), owa, err_msg=f"warmstart step {s}")
             info = gb.get_info()
             np.testing.assert_array_equal(info["ncon"].cpu().numpy(), onc, err_msg=f"ncon step {s}")
+            if mc.ntouch > 0:
+                gt = gb.get_touch().cpu().numpy()
+                ot = np.stack([ob.diag(i)["touch"][:mc.ntouch] for i in range(n)])
+                np.testing.assert_array_equal(gt, ot, err_msg=f"touch step {s}")
+                max_touch[0] = max(max_touch[0], float(ot.max()))
     assert max_dq <= 1e-5
     gb.ovf = gb.overflow_count()
+    gb.max_touch = max_touch[0]
     gb.close()
     return gb
 
@@ -127,3 +134,45 @@ def test_ctrl_raw():
 def test_gym_v2_1000_steps():
     """north_star: qpos within 1e-5 after 1000 steps (here: bit-exact)."""
     _run_pair("main", 0, 128, 1000, _gym_actions, check_every=100)
+
+
+def test_move_l_mug_scripted_pick():
+    """C3 semantics (controller/move_l_mug.py): closed-loop pid_task_ctrl along per-env
+    build_traj_l_pick_place rows, one mj_step per row, through the pick and most of the lift
+    segment; GPU vs oracle bit-exact on state, contacts, touch sensors and the task-space obs,
+    and the scripted grasp really happens: both pads on the mug (obs[23] robust grasp) and the
+    mug lifted off the table."""
+    torch = _torch()
+    from oracle import pyoracle as po
+    from ur3e_amd import runtime as rt
+    from ur3e_amd.controller.move_l_mug import MoveLMug, task_space_state
+    n = 16
+    drv = MoveLMug(n, reset_mode="low", seed=5)
+    gb = drv.batch
+    ob = po.OracleBatch(gb.model_c, _oracle_cfg(po, gb.cfg), n)
+    np.testing.assert_array_equal(gb.obs.cpu().numpy(), ob.obs)
+    max_touch = 0.0
+    grasped = np.zeros(n, dtype=bool)
+    z0 = gb.obs[:, 5].cpu().numpy().copy()
+    steps = 3000
+    for s in range(steps):
+        row = drv.step()
+        o_obs = ob.step(row.cpu().numpy())[0]
+        if s % 250 == 0 or s == steps - 1:
+            torch.cuda.synchronize()
+            qp, qv, wa = gb.get_state()
+            oqp, oqv, owa, onc = ob.get_state()
+            np.testing.assert_array_equal(qp.cpu().numpy(), oqp, err_msg=f"qpos row {s}")
+            np.testing.assert_array_equal(qv.cpu().numpy(), oqv, err_msg=f"qvel row {s}")
+            np.testing.assert_array_equal(gb.get_info()["ncon"].cpu().numpy(), onc, err_msg=f"ncon row {s}")
+            np.testing.assert_array_equal(gb.obs.cpu().numpy(), o_obs, err_msg=f"obs row {s}")
+            gt = gb.get_touch().cpu().numpy()
+            ot = np.stack([ob.diag(i)["touch"][:2] for i in range(n)])
+            np.testing.assert_array_equal(gt, ot, err_msg=f"touch row {s}")
+            max_touch = max(max_touch, float(gt.max()))
+            grasped |= o_obs[:, 23] == 1.0
+    assert grasped.sum() >= n // 4
+    assert (gb.obs[:, 5].cpu().numpy() - z0).max() > 0.01
+    st = task_space_state(gb)
+    assert st.shape == (n, 7)
+    drv.close()

@@ -1,0 +1,112 @@
+"""Batched scripted pick-and-place: controller/move_l_mug.py:16-98 for N envs on one GPU.
+
+Per env, as the reference's main():
+  reset_with_mug(m, d, reset_mode, keyframe="down")            gym_utils.py:82-93
+  init_r = get_site_xrotvec(tcp); start = get_task_space_state  controller_func.py:191-200
+  pick  = [get_mug_xpos (handle_site), init_r, 0.5]
+  place = [get_ghost_xpos, init_r, 1]
+  traj  = build_traj_l_pick_place(start, [pick, place])        build_traj.py:28-59 (7200 rows)
+  for t: u = pid_task_ctrl(traj[t]); mj_step; traj_true[t] = get_task_space_state
+
+The controller and mj_step run inside the step library (task UR3E_TASK_TRAJ_L, one
+substep per row); trajectory rows are evaluated on the GPU (PickPlaceTorch).  The
+task-space state uses the stale-kinematics carry (tcp site pose of the last forward),
+scipy's matrix -> rotvec conversion (as utils/utils.py:158-162 does), and the pad touch
+sensors compared lexicographically with (0.1, 0.1) (utils/utils.py:238-245).
+
+Out of scope: the viewer, CSV/plot logging (controller/aux.py cleanup).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .build_traj import PickPlaceTorch
+
+NOISE = {"deterministic": 0, "high": 1, "med": 2, "low": 3}
+
+
+def task_space_state(batch):
+    """get_task_space_state for all envs: [N, 7] = tcp xpos, tcp rotvec, boolean grasp contact."""
+    import torch
+    from scipy.spatial.transform import Rotation as R
+    carry = batch.get_carry()
+    xpos = carry[:, 0:3]
+    xmat = carry[:, 3:12].cpu().numpy().reshape(-1, 3, 3)
+    rotvec = torch.from_numpy(R.from_matrix(xmat).as_rotvec()).to(carry.device)
+    touch = batch.get_touch()
+    # sensor order follows main.xml <sensor>: right_pad1_contact, left_pad1_contact; get_grasp_contact
+    # returns (left, right)
+    li, ri = batch.touch_index("left"), batch.touch_index("right")
+    left, right = touch[:, li], touch[:, ri]
+    # tuple comparison (left, right) > (0.1, 0.1)
+    grip = (left > 0.1) | ((left == 0.1) & (right > 0.1))
+    return torch.cat([xpos, rotvec, grip.to(torch.float64)[:, None]], dim=1)
+
+
+class MoveLMug:
+    """N scripted pick-and-place episodes stepping in lock-step."""
+
+    def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
+                 envs_per_block: int = 0):
+        import torch
+        from .. import runtime as rt
+        self.torch = torch
+        md, mc = rt.load_model("main")
+        self.md = md
+        cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
+                             reset_noise=NOISE[reset_mode], reset_key=md["id_key_down"], model=md, seed=seed,
+                             envs_per_block=envs_per_block)
+        self.batch = rt.Batch(mc, cfg, n_envs, device=device)   # reset_with_mug (keyframe + forward)
+        obs = self.batch.obs
+        start = task_space_state(self.batch)
+        init_r = start[:, 3:6]
+        n = n_envs
+        half = torch.full((n, 1), 0.5, dtype=torch.float64, device=obs.device)
+        one = torch.ones((n, 1), dtype=torch.float64, device=obs.device)
+        self.pick = torch.cat([obs[:, 3:6], init_r, half], dim=1)
+        self.place = torch.cat([obs[:, 6:9], init_r, one], dim=1)
+        self.start = start
+        self.traj = PickPlaceTorch(start, self.pick, self.place)
+        self.T = self.traj.T
+        self.t = 0
+
+    def step(self):
+        """One trajectory row for all envs: pid_task_ctrl + 1 mj_step."""
+        row = self.traj.row(self.t)
+        self.batch.step(row)
+        self.t += 1
+        return row
+
+    def run(self, steps: int | None = None, record_every: int = 0):
+        """Run `steps` rows (default: the whole 7200-row trajectory).  With record_every > 0,
+        returns traj_true samples {t: [N, 7]} taken every record_every steps."""
+        steps = self.T if steps is None else min(steps, self.T - self.t)
+        rec = {}
+        for _ in range(steps):
+            self.step()
+            if record_every and self.t % record_every == 0:
+                rec[self.t] = task_space_state(self.batch)
+        return rec
+
+    def close(self):
+        self.batch.close()
+
+
+def main(n_envs: int = 4096, steps: int | None = None):  # pragma: no cover - GPU script
+    import time
+    import torch
+    drv = MoveLMug(n_envs)
+    t0 = time.perf_counter()
+    drv.run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = task_space_state(drv.batch)
+    obs = drv.batch.obs
+    print(f"{n_envs} envs x {drv.t} rows: {n_envs * drv.t / dt:.0f} env-steps/s; "
+          f"mean handle z {obs[:, 5].mean().item():.4f}; grasp flag mean {st[:, 6].mean().item():.3f}")
+    drv.close()
+
+
+if __name__ == "__main__":  # pragma: no cover
+    import sys
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 4096, int(sys.argv[2]) if len(sys.argv) > 2 else None)

@@ -296,6 +296,7 @@ struct KState {
   double* ep_return;
   int* ncon;
   int* nwarn;
+  double* touch; /* [env][UR3E_MAXTOUCH] touch sensors after the last forward */
 };
 
 struct KConfig {
@@ -304,8 +305,17 @@ struct KConfig {
   int env_id_offset;
   int epb;
   int tier_con_cap;
+  int obs_sites; /* model has tcp / handle_site / ghost: the scripted tasks also emit the 24-d obs */
   KGains gains;
 };
+
+/* gym_utils.get_mug_xpos_noise (gym_utils.py:48-60): x ~ U[0, 0.02] for every magnitude, y bounds by
+   magnitude (reset_noise 1 = "high", 2 = "med", 3 = "low") */
+KD void k_noise_ybounds(int mag, double* lo, double* hi) {
+  if (mag == 2) { *lo = -0.2; *hi = 0.1; }
+  else if (mag == 3) { *lo = -0.1; *hi = 0.01; }
+  else { *lo = -0.25; *hi = 0.2; }
+}
 
 KD size_t SQ(const KState& s, int k, int e) { return (size_t)k * s.fs + (size_t)e * s.es_q; }
 KD size_t SV(const KState& s, int k, int e) { return (size_t)k * s.fs + (size_t)e * s.es_v; }
@@ -325,6 +335,7 @@ KD void k_store(KModel m, const KState& s, int e, const KData* d, const double* 
   for (int k = 0; k < NCARRY; k++) s.carry[SC(s, k, e)] = carry[k];
   s.ncon[e] = d->ncon;
   s.nwarn[e] = d->nwarn;
+  for (int k = 0; k < UR3E_MAXTOUCH; k++) s.touch[(size_t)e * UR3E_MAXTOUCH + k] = d->touch[k];
 }
 
 /* reset one env in registers/scratch: keyframe (+ mug noise), forward, obs, carry */
@@ -342,8 +353,10 @@ KD void k_reset_env(KModel m, const KConfig& c, const KState& s, int e, KData* d
     unsigned int gid = (unsigned int)(c.env_id_offset + e);
     double u0 = k_uniform01(c.seed, gid, ep, 0);
     double u1 = k_uniform01(c.seed, gid, ep, 1);
+    double ylo, yhi;
+    k_noise_ybounds(c.reset_noise, &ylo, &yhi);
     d->qpos[14] += 0.0 + (0.02 - 0.0) * u0;
-    d->qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+    d->qpos[15] += ylo + (yhi - ylo) * u1;
   }
   d->nwarn = 0;
   k_forward(m, d);
@@ -351,7 +364,7 @@ KD void k_reset_env(KModel m, const KConfig& c, const KState& s, int e, KData* d
   s.ep_len[e] = 0;
   s.ep_return[e] = 0;
   s.episode[e] = ep + 1;
-  if (c.task == UR3E_TASK_GYM_V2) k_obs_v2(m, d, obs);
+  if (c.task == UR3E_TASK_GYM_V2 || c.obs_sites) k_obs_v2(m, d, obs);
   k_make_carry(m, d, carry);
 }
 
@@ -372,7 +385,7 @@ __global__ __launch_bounds__(64) void k_env_reset(const ur3e_model_t* __restrict
   double obs[24], carry[NCARRY];
   k_reset_env(m, c, s, e, &d, obs, carry);
   k_store(m, s, e, &d, carry);
-  if (obs_out && c.task == UR3E_TASK_GYM_V2)
+  if (obs_out && (c.task == UR3E_TASK_GYM_V2 || c.obs_sites))
     for (int k = 0; k < 24; k++) obs_out[(size_t)e * 24 + k] = obs[k];
 }
 
@@ -419,6 +432,11 @@ __global__ __launch_bounds__(64) void k_env_step(const ur3e_model_t* __restrict_
   if (c.task != UR3E_TASK_GYM_V2) {
     s.ep_len[e] += 1;
     k_store(m, s, e, &d, carry);
+    if (obs_out && c.obs_sites) {
+      double ob[24];
+      k_obs_v2(m, &d, ob);
+      for (int k = 0; k < 24; k++) obs_out[(size_t)e * 24 + k] = ob[k];
+    }
     return;
   }
   double obs[24];
@@ -602,6 +620,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
+  for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
@@ -614,9 +633,9 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   if (c.task == UR3E_TASK_GYM_V2) {
     if (stepped && o.did_reset && tobs_out)
       for (int k = tid; k < 24; k += NT) tobs_out[(size_t)e * 24 + k] = o.tobs[k];
-    if (obs_out)
-      for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
   }
+  if (obs_out && (c.task == UR3E_TASK_GYM_V2 || c.obs_sites))
+    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
 }
 
 /* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
@@ -633,8 +652,10 @@ WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
       unsigned int gid = (unsigned int)(c.env_id_offset + e);
       double u0 = k_uniform01(c.seed, gid, ep, 0);
       double u1 = k_uniform01(c.seed, gid, ep, 1);
+      double ylo, yhi;
+      k_noise_ybounds(c.reset_noise, &ylo, &yhi);
       s.qpos[14] += 0.0 + (0.02 - 0.0) * u0;
-      s.qpos[15] += -0.25 + (0.2 - -0.25) * u1;
+      s.qpos[15] += ylo + (yhi - ylo) * u1;
     }
     s.nwarn = 0;
     o.t = 0;
@@ -648,7 +669,7 @@ WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
 template <int NT, class KS>
 WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c, KS& s, WOut& o) {
   const int tid = threadIdx.x;
-  if (tid == 0 && c.task == UR3E_TASK_GYM_V2) w_obs_v2(m, s, o.obs);
+  if (tid == 0 && (c.task == UR3E_TASK_GYM_V2 || c.obs_sites)) w_obs_v2(m, s, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
 }
@@ -729,7 +750,10 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     w_make_carry<NT>(m, pl, s, o.carry);
     SYNC();
     if (c.task != UR3E_TASK_GYM_V2) {
-      if (tid == 0) { o.t += 1; o.ep_len += 1; }
+      if (tid == 0) {
+        o.t += 1; o.ep_len += 1;
+        if (c.obs_sites) w_obs_v2(m, s, o.obs);
+      }
       SYNC();
       return true;
     }
@@ -871,6 +895,12 @@ __global__ void k_env_get_state(int nq, int nv, KState s, double* __restrict__ q
     for (int k = 0; k < nv; k++) warm[(size_t)e * nv + k] = s.warm[SV(s, k, e)];
 }
 
+__global__ void k_env_get_touch(KState s, int ntouch, double* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  for (int k = 0; k < ntouch; k++) out[(size_t)e * ntouch + k] = s.touch[(size_t)e * UR3E_MAXTOUCH + k];
+}
+
 __global__ void k_env_get_info(KState s, int* ncon, int* ep_len, double* ep_ret, int* nwarn) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= s.n) return;
@@ -1007,6 +1037,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.env_id_offset = cfg->env_id_offset;
   c.epb = cfg->envs_per_block > 0 && cfg->envs_per_block <= 64 ? cfg->envs_per_block : 16;
   c.tier_con_cap = cfg->tier_con_cap;
+  c.obs_sites = model->id_site_tcp >= 0 && model->id_site_handle >= 0 && model->id_body_ghost >= 0;
   KPlan plan;
   build_plan(model, &plan);
   b->main_tree = model->nv == UR3E_MAIN_NV;
@@ -1035,6 +1066,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMalloc(&s.ep_return, sizeof(double) * nd));
   HIPCHK(hipMalloc(&s.ncon, sizeof(int) * nd));
   HIPCHK(hipMalloc(&s.nwarn, sizeof(int) * nd));
+  HIPCHK(hipMalloc(&s.touch, sizeof(double) * nd * UR3E_MAXTOUCH));
+  HIPCHK(hipMemset(s.touch, 0, sizeof(double) * nd * UR3E_MAXTOUCH));
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
@@ -1056,7 +1089,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
   void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
-                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->d_ovf_list, b->d_ovf_count,
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->d_ovf_list, b->d_ovf_count,
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   (void)hipEventDestroy(b->ev0);
@@ -1209,6 +1242,30 @@ extern "C" int ur3e_debug_stage_bench(ur3e_batch_t* b, int stage, int reps, unsi
   return UR3E_OK;
 }
 #endif
+
+__global__ void k_env_get_carry(KState s, double* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  for (int k = 0; k < NCARRY; k++) out[(size_t)e * NCARRY + k] = s.carry[SC(s, k, e)];
+}
+
+extern "C" int ur3e_batch_get_carry(ur3e_batch_t* b, double* d_carry, void* stream) {
+  if (!b || !d_carry) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_get_carry, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st, d_carry);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream) {
+  if (!b || !d_touch) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  if (b->host_model.ntouch > 0)
+    hipLaunchKernelGGL(k_env_get_touch, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
+                       b->host_model.ntouch, d_touch);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
 
 /* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */
 extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {

@@ -109,6 +109,7 @@ struct KData {
   double efc_aref[K_MAXEFC];
   double efc_floss[K_MAXEFC];
   double efc_force[K_MAXEFC];
+  double touch[UR3E_MAXTOUCH];
   double jar[K_MAXEFC];
   double Jv[K_MAXEFC];
   /* velocity stage */
@@ -1414,6 +1415,48 @@ KDN void k_solve_newton(KModel m, KData* d) {
 /* ================================================================== */
 /* forward / step                                                      */
 /* ================================================================== */
+/* touch sensor ray test (mj_sensorAcc mjSENS_TOUCH): does the ray from p along dir hit the site box */
+KD int k_ray_box_hit(const double sp[3], const double sm[9], const double ss[3], const double p[3],
+                     const double dir[3]) {
+  double lp[3], ld[3], dp[3] = {p[0] - sp[0], p[1] - sp[1], p[2] - sp[2]};
+  k_mat_t_vec3(lp, sm, dp);
+  k_mat_t_vec3(ld, sm, dir);
+  double tmin = 0.0, tmax = 1e300;
+  for (int k = 0; k < 3; k++) {
+    if (fabs(ld[k]) < K_MINVAL) {
+      if (lp[k] < -ss[k] || lp[k] > ss[k]) return 0;
+    } else {
+      double t1 = (-ss[k] - lp[k]) / ld[k], t2 = (ss[k] - lp[k]) / ld[k];
+      if (t1 > t2) { double tt = t1; t1 = t2; t2 = tt; }
+      if (t1 > tmin) tmin = t1;
+      if (t2 < tmax) tmax = t2;
+      if (tmin > tmax) return 0;
+    }
+  }
+  return 1;
+}
+
+/* touch sensors, oracle sensor_touch (oracle/ur3e_oracle.c) */
+KD void k_touch(KModel m, KData* d) {
+  for (int s = 0; s < m->ntouch; s++) {
+    int site = m->touch_site[s];
+    int body = m->site_bodyid[site];
+    double sum = 0;
+    for (int ci = 0; ci < d->ncon; ci++) {
+      const KContact* c = d->contact + ci;
+      if (c->efc_address < 0) continue;
+      int b1 = m->geom_bodyid[c->geom1], b2 = m->geom_bodyid[c->geom2];
+      if (body != b1 && body != b2) continue;
+      double fn = d->efc_force[c->efc_address];
+      if (fn <= 0) continue;
+      double ray[3] = {c->frame[0], c->frame[1], c->frame[2]};
+      if (body == b2) { ray[0] = -ray[0]; ray[1] = -ray[1]; ray[2] = -ray[2]; }
+      if (k_ray_box_hit(d->site_xpos[site], d->site_xmat[site], m->site_size[site], c->pos, ray)) sum += fn;
+    }
+    d->touch[s] = sum;
+  }
+}
+
 KDN void k_forward(KModel m, KData* d) {
   const int nv = m->nv;
   k_kinematics(m, d);
@@ -1433,6 +1476,7 @@ KDN void k_forward(KModel m, KData* d) {
   for (int k = 0; k < nv; k++) d->qfrc_smooth[k] = d->qfrc_passive[k] - d->qfrc_bias[k] + qfrc_act[k];
   k_solve_tree(m, d->qLD, d->qLDiagInv, d->qacc_smooth, d->qfrc_smooth);
   k_solve_newton(m, d);
+  k_touch(m, d);
 }
 
 KD int k_is_bad(double x) { return x != x || x > K_MAXVAL || x < -K_MAXVAL; }

@@ -101,6 +101,7 @@ struct KSX {
   double efc_force[ME], jar[ME], Jv[ME];
   int efc_type[ME], efc_id[ME], efc_state[ME], rowflag[ME], efc_grp[ME];
   int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
+  double touch[UR3E_MAXTOUCH];
   /* scalars */
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
@@ -1386,6 +1387,29 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   else
     w_solve_newton<NT>(m, s);
   WT(15);
+  /* touch sensors (lane = sensor), oracle sensor_touch */
+  if (tid < m->ntouch) {
+    const int site = m->touch_site[tid];
+    const int body = m->site_bodyid[site];
+    double sp[3], sm[9], ss[3];
+    for (int k = 0; k < 3; k++) { sp[k] = s.site_xpos[site][k]; ss[k] = m->site_size[site][k]; }
+    for (int k = 0; k < 9; k++) sm[k] = s.site_xmat[site][k];
+    double sum = 0;
+    for (int ci = 0; ci < s.ncon; ci++) {
+      const int adr = s.con_efc[ci];
+      if (adr < 0) continue;
+      const int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+      if (body != b1 && body != b2) continue;
+      const double fn = s.efc_force[adr];
+      if (fn <= 0) continue;
+      double ray[3] = {s.con_frame[ci][0], s.con_frame[ci][1], s.con_frame[ci][2]};
+      if (body == b2) { ray[0] = -ray[0]; ray[1] = -ray[1]; ray[2] = -ray[2]; }
+      double cp[3] = {s.con_pos[ci][0], s.con_pos[ci][1], s.con_pos[ci][2]};
+      if (k_ray_box_hit(sp, sm, ss, cp, ray)) sum += fn;
+    }
+    s.touch[tid] = sum;
+  }
+  SYNC();
 }
 
 /* mj_step pieces around the forward pass, so a caller can keep ONE inlined copy of w_forward

@@ -564,6 +564,7 @@ WD void r_solve_newton(KModel m, KS& s) {
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
+  if (lane < s.nefc) s.efc_force[lane] = w.force; /* touch sensors read the contact normal forces */
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }

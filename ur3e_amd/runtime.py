@@ -62,6 +62,8 @@ def load_library():
     L.ur3e_batch_get_info.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ur3e_batch_last_step_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
+    L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu"):
         getattr(L, f).argtypes = [vp]
     _lib = L
@@ -88,7 +90,9 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.frame_skip = frame_skip
     c.max_episode_steps = max_episode_steps
     c.auto_reset = int(auto_reset)
-    c.reset_noise = int(reset_noise)
+    # True/1: "high" (ur3e-v2); 2 "med"; 3 "low"; also accepts the reference's names
+    c.reset_noise = {"high": 1, "med": 2, "low": 3, None: 0, "deterministic": 0}.get(reset_noise, None) \
+        if (reset_noise is None or isinstance(reset_noise, str)) else int(reset_noise)
     if reset_key is None:
         reset_key = model["id_key_down"] if model is not None else -1
     c.reset_key = reset_key
@@ -187,6 +191,27 @@ class Batch:
         nw = t.empty(self.n, dtype=t.int32, device=self.device)
         _check(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
         return dict(ncon=nc, ep_len=el, ep_return=er, nwarn=nw)
+
+    def get_carry(self):
+        """[N, 54] stale-kinematics snapshot: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6]."""
+        out = self.torch.empty((self.n, 54), dtype=self.torch.float64, device=self.device)
+        _check(self.L.ur3e_batch_get_carry(self.h, _ptr(out), self._stream()))
+        return out
+
+    def touch_index(self, side: str) -> int:
+        """Column of get_touch() for the left / right pad sensor (site on the lpad / rpad body)."""
+        body = self.model_c.id_body_lpad if side == "left" else self.model_c.id_body_rpad
+        for k in range(self.model_c.ntouch):
+            if self.model_c.site_bodyid[self.model_c.touch_site[k]] == body:
+                return k
+        raise KeyError(side)
+
+    def get_touch(self):
+        """Touch sensors [N, ntouch] after the last forward (mjSENS_TOUCH on the pad sites)."""
+        nt = max(self.model_c.ntouch, 1)
+        out = self.torch.zeros((self.n, nt), dtype=self.torch.float64, device=self.device)
+        _check(self.L.ur3e_batch_get_touch(self.h, _ptr(out), self._stream()))
+        return out[:, :self.model_c.ntouch]
 
     def overflow_count(self) -> int:
         """Env-steps the compact tier handed to the full-capacity tier since create."""
