@@ -46,6 +46,11 @@ extern "C" {
 #define UR3E_TASK_TRAJ_L 1  /* action [N,7] task-space trajectory row: pid_task_ctrl */
 #define UR3E_TASK_MOVE_J 2  /* action [N,7] joint targets + grip: move_j PD */
 #define UR3E_TASK_CTRL 3    /* action [N,nu] raw actuator controls */
+/* the other registered gymnasium ids (gymnasium_env/register_envs.py:4-20); workgroup-per-env
+   layouts only (envs_per_block <= 0) */
+#define UR3E_TASK_GYM_V0 4          /* ur3e-v0 (ur3e_env.py): action [N,4], obs [N,13], T = 500 */
+#define UR3E_TASK_IMIT_INDIRECT 5   /* imitation_indirect-v0: action [N,4], obs [N,24], reward -1 */
+#define UR3E_TASK_IMIT_DIRECT 6     /* imitation_direct-v0: action [N,nu] ctrl, obs [N,13], reward -1 */
 
 /* error codes */
 #define UR3E_OK 0
@@ -121,6 +126,9 @@ int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream);
 
 /* envs the compact tier handed to the full-capacity tier since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
+
+/* observation width of the handle's task (24 or 13) */
+int ur3e_batch_obs_dim(const ur3e_batch_t* b);
 
 /* sizes */
 int ur3e_batch_num_envs(const ur3e_batch_t* b);

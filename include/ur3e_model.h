@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define UR3E_MODEL_VERSION 3
+#define UR3E_MODEL_VERSION 4
 
 #define UR3E_MAXBODY 28
 #define UR3E_MAXJNT 16
@@ -197,6 +197,10 @@ typedef struct ur3e_model_t {
   unsigned int mask_gripper_bodies; /* robotiq_base_mount and descendants */
   /* get_mug_toppled threshold: max(dx, dy) of the first fish geom */
   double fish_topple_z;
+  /* gym_utils.get_table_collision's table body (-1 when absent) */
+  int id_body_table;
+  /* get_body_size(m, "fish")[-1]: half height of the first fish geom (ur3e_env.py compute_reward) */
+  double fish_half_z;
 } ur3e_model_t;
 
 #ifdef __cplusplus

@@ -55,18 +55,19 @@ class OracleBatch:
         self.n = n_envs
         self.nq, self.nv = model_c.nq, model_c.nv
         self.buf = ctypes.create_string_buffer(self.L.ur3o_sizeof_env() * n_envs)
-        self.obs = np.zeros((n_envs, 24))
+        self.od = self.L.ur3o_obs_dim(ctypes.c_int(cfg.task))
+        self.obs = np.zeros((n_envs, self.od))
         self.L.ur3o_batch_init(ctypes.byref(self.m), ctypes.byref(self.cfg), ctypes.c_int(n_envs), self.buf,
                                _p(self.obs))
 
     def step(self, actions: np.ndarray):
         actions = np.ascontiguousarray(actions, dtype=np.float64)
         n = self.n
-        obs = np.zeros((n, 24))
+        obs = np.zeros((n, self.od))
         rew = np.zeros(n)
         term = np.zeros(n, np.uint8)
         trunc = np.zeros(n, np.uint8)
-        tobs = np.zeros((n, 24))
+        tobs = np.zeros((n, self.od))
         self.L.ur3o_batch_step(ctypes.byref(self.m), ctypes.byref(self.cfg), ctypes.c_int(n), self.buf,
                                _p(actions), ctypes.c_int(actions.shape[1]), _p(obs), _p(rew), _p(term),
                                _p(trunc), _p(tobs))
@@ -111,6 +112,20 @@ def forward_state(model_c, qpos, qvel=None):
     L.ur3o_forward_state(ctypes.byref(model_c), _p(qpos), _p(qvel), _p(sx), _p(sm), _p(bias), _p(M),
                          ctypes.byref(ncon))
     return dict(site_xpos=sx, site_xmat=sm, qfrc_bias=bias, qM=M, ncon=ncon.value)
+
+
+def v0_epilogue(model_c, pairs, obs13, act4):
+    """ur3e-v0 reward / termination / table collision for a synthetic contact list."""
+    L = lib()
+    pairs = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
+    g1 = np.ascontiguousarray(pairs[:, 0])
+    g2 = np.ascontiguousarray(pairs[:, 1])
+    r = ctypes.c_double()
+    oi = np.zeros(2, np.int32)
+    L.ur3o_v0_epilogue(ctypes.byref(model_c), ctypes.c_int(len(pairs)), _p(g1), _p(g2),
+                       _p(np.ascontiguousarray(obs13, dtype=np.float64)),
+                       _p(np.ascontiguousarray(act4, dtype=np.float64)), ctypes.byref(r), _p(oi))
+    return r.value, int(oi[0]), int(oi[1])
 
 
 def rot_err(xmat, target):

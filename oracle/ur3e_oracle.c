@@ -1801,6 +1801,99 @@ int ur3o_termination_v2(const ur3e_model_t* m, const ur3o_data* d, const double 
 }
 
 /* ===================================================================== */
+/* UR3eEnv (ur3e-v0) and imitation-env epilogues                           */
+/* ===================================================================== */
+int ur3o_table_collision(const ur3e_model_t* m, const ur3o_data* d) {
+  /* gym_utils.py:174-197: any gripper-tree body touching the table body */
+  for (int ci = 0; ci < d->ncon; ci++) {
+    int b1 = m->geom_bodyid[d->contact[ci].geom1], b2 = m->geom_bodyid[d->contact[ci].geom2];
+    int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+    if ((g1 && b2 == m->id_body_table) || (g2 && b1 == m->id_body_table)) return 1;
+  }
+  return 0;
+}
+
+void ur3o_obs_v0(const ur3e_model_t* m, const ur3o_data* d, double obs[13]) {
+  /* ur3e_env.py _get_obs: tcp, handle_site, ghost, block grasp state, right_pad1_site */
+  const double* tcp = d->site_xpos[m->id_site_tcp];
+  const double* mug = d->site_xpos[m->id_site_handle];
+  const double* gh = d->xpos[m->id_body_ghost];
+  const double* pad = d->site_xpos[m->id_site_rpad];
+  for (int k = 0; k < 3; k++) { obs[k] = tcp[k]; obs[3 + k] = mug[k]; obs[6 + k] = gh[k]; obs[10 + k] = pad[k]; }
+  obs[9] = (double)ur3o_block_grasp_state(m, d);
+}
+
+void ur3o_obs_direct(const ur3e_model_t* m, const ur3o_data* d, double obs[13]) {
+  /* imitation_env_direct.py _get_obs: tcp, handle_site, ghost, block grasp state, tcp linear velocity */
+  const double* tcp = d->site_xpos[m->id_site_tcp];
+  const double* mug = d->site_xpos[m->id_site_handle];
+  const double* gh = d->xpos[m->id_body_ghost];
+  double vt[6];
+  ur3o_site_velocity(m, d, m->id_site_tcp, vt);
+  for (int k = 0; k < 3; k++) { obs[k] = tcp[k]; obs[3 + k] = mug[k]; obs[6 + k] = gh[k]; obs[10 + k] = vt[3 + k]; }
+  obs[9] = (double)ur3o_block_grasp_state(m, d);
+}
+
+static double sq(double x) { return x * x; }
+
+double ur3o_reward_v0(const ur3e_model_t* m, const ur3o_data* d, const double obs[13], const double act[4]) {
+  /* ur3e_env.py:compute_reward (the per-20-step print is dropped) */
+  const double* gripper_pos = obs;
+  const double* block_center = obs + 3;
+  const double* target_pos = obs + 6;
+  double grasp_state = obs[9];
+  const double* pad_pos = obs + 10;
+  double block_half_height = m->fish_half_z;
+  double block_top_z = block_center[2] + block_half_height;
+  double block_bottom_z = block_center[2] - block_half_height;
+  double pad_to_block_top = pad_pos[2] - block_top_z;
+  double gripper_to_block_center = gripper_pos[2] - block_center[2];
+  double hx = gripper_pos[0] - block_center[0], hy = gripper_pos[1] - block_center[1];
+  double horizontal_error = sqrt(hx * hx + hy * hy);
+  int valid_grasp = grasp_state == 2 && fabs(pad_to_block_top) < 0.04 && horizontal_error < 0.03;
+  double ideal_height_above = 0.5;
+  double height_error = gripper_to_block_center - ideal_height_above;
+  double z_tol = 0.1;
+  double descent_reward = 1 * ((1 / z_tol) * (height_error + z_tol) * ur3e_exp(-(1 / z_tol) * height_error));
+  double grasp_readiness = ur3e_exp(-sq(horizontal_error)) * ur3e_exp(-sq(pad_to_block_top)) *
+                           ur3e_exp(-sq(height_error)) * 100 * ur3e_exp(-sq(act[3]));
+  double alignment_reward = 4 * ur3e_exp(-60 * sq(horizontal_error));
+  double grip_strength = act[3];
+  double g2 = grasp_state == 2 ? 1.0 : 0.0, g1 = grasp_state >= 1 ? 1.0 : 0.0;
+  double grasp_reward = 5.5 * g1 + 8.5 * g2 + 23.5 * grip_strength * grasp_readiness + 28.5 * g2 * grasp_readiness +
+                        11.5 * g2 * grasp_readiness * ur3e_tanh(8 * grip_strength);
+  double lift_reward = 12 * g2 * ur3e_tanh(4 * block_bottom_z);
+  double px = block_center[0] - target_pos[0], py = block_center[1] - target_pos[1],
+         pz = block_center[2] - target_pos[2];
+  double d_place = sqrt(px * px + py * py + pz * pz);
+  double placement_reward = -2 * d_place + 20 * ur3e_exp(-70 * sq(d_place));
+  if (d_place < 0.05 && valid_grasp) placement_reward += 40;
+  double hh = block_center[2] - gripper_pos[2] + 0.5;
+  double dh = -100000000000.0 * (hh * hh * hh);
+  double dangerous_height_penalty = dh < 0 ? dh : 0;
+  double p2b = pad_to_block_top > 0 ? pad_to_block_top : 0;
+  double penalties = -40 * ur3o_self_collision(m, d) + -25 * ur3o_table_collision(m, d) +
+                     -8 * (block_center[2] <= m->fish_topple_z) + -4 * p2b + dangerous_height_penalty;
+  double action_reward = 700.5 * grip_strength * grasp_readiness;
+  double contact_achievement_bonus = 1700.5 * g2 * grasp_readiness * ur3e_tanh(10 * grip_strength);
+  return descent_reward + alignment_reward + grasp_reward + lift_reward + placement_reward + action_reward +
+         contact_achievement_bonus + penalties;
+}
+
+int ur3o_termination_v0(const ur3e_model_t* m, const ur3o_data* d, const double obs[13]) {
+  /* ur3e_env.py:_check_termination */
+  double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
+  double ex = obs[3] - obs[6], ey = obs[4] - obs[7], ez = obs[5] - obs[8];
+  double d_pick = sqrt(dx * dx + dy * dy + dz * dz);
+  double d_place = sqrt(ex * ex + ey * ey + ez * ez);
+  if (d_place < 0.005) return 1;
+  if (1 < d_pick) return 1;
+  if (ur3o_self_collision(m, d)) return 1;
+  if (obs[5] <= m->fish_topple_z) return 1;
+  return 0;
+}
+
+/* ===================================================================== */
 /* Philox4x32-10                                                           */
 /* ===================================================================== */
 void ur3o_philox4x32(const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]) {

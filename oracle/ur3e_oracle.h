@@ -178,6 +178,12 @@ void ur3o_move_l_ctrl(const ur3e_model_t* m, const ur3o_data* d, const double tr
 
 /* ---- UR3eEnv2 epilogue ---- */
 void ur3o_obs_v2(const ur3e_model_t* m, const ur3o_data* d, double obs[24]);
+/* ur3e-v0 / imitation epilogues (gymnasium_env/envs/ur3e_env.py, imitation_env_direct.py) */
+int ur3o_table_collision(const ur3e_model_t* m, const ur3o_data* d);
+void ur3o_obs_v0(const ur3e_model_t* m, const ur3o_data* d, double obs[13]);
+void ur3o_obs_direct(const ur3e_model_t* m, const ur3o_data* d, double obs[13]);
+double ur3o_reward_v0(const ur3e_model_t* m, const ur3o_data* d, const double obs[13], const double act[4]);
+int ur3o_termination_v0(const ur3e_model_t* m, const ur3o_data* d, const double obs[13]);
 double ur3o_reward_v2(const double obs[24], const double act[4]);
 int ur3o_termination_v2(const ur3e_model_t* m, const ur3o_data* d, const double obs[24]);
 

@@ -40,6 +40,16 @@ static int has_obs_sites(const ur3e_model_t* m) {
   return m->id_site_tcp >= 0 && m->id_site_handle >= 0 && m->id_body_ghost >= 0;
 }
 
+/* tasks (include/ur3e_batch.h): 0 gym v2, 1 traj_l, 2 move_j, 3 ctrl, 4 gym v0, 5 imitation
+   indirect, 6 imitation direct */
+static int is_gym(int task) { return task == 0 || task >= 4; }
+int ur3o_obs_dim(int task) { return (task == 4 || task == 6) ? 13 : 24; }
+static void task_obs(const ur3e_model_t* m, const ur3o_data* d, int task, double* obs) {
+  if (task == 4) ur3o_obs_v0(m, d, obs);
+  else if (task == 6) ur3o_obs_direct(m, d, obs);
+  else ur3o_obs_v2(m, d, obs);
+}
+
 static void gains_from_cfg(const ur3o_config* c, ur3o_task_gains* tg, ur3o_joint_gains* jg) {
   for (int k = 0; k < 3; k++) {
     tg->kp_pos[k] = c->task_gains[k];
@@ -77,7 +87,7 @@ static void env_reset(const ur3e_model_t* m, const ur3o_config* c, ur3o_env* e, 
   e->ep_return = 0;
   e->ep_len = 0;
   e->episode++;
-  if (obs && (c->task == 0 || has_obs_sites(m))) ur3o_obs_v2(m, d, obs);
+  if (obs && (is_gym(c->task) || has_obs_sites(m))) task_obs(m, d, c->task, obs);
 }
 
 /* envs: array of n ur3o_env (opaque to python: allocate n*ur3o_sizeof_env()) */
@@ -85,7 +95,7 @@ void ur3o_batch_init(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < n; i++) {
     ur3o_env_init(m, &envs[i], c->seed, (unsigned int)(c->env_id_offset + i));
-    env_reset(m, c, &envs[i], obs ? obs + 24 * (size_t)i : 0);
+    env_reset(m, c, &envs[i], obs ? obs + (size_t)ur3o_obs_dim(c->task) * i : 0);
   }
 }
 
@@ -106,6 +116,7 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
     ur3o_data* d = &e->d;
     const double* a = actions + (size_t)adim * i;
     double ctrl[UR3E_MAXU];
+    const int od = ur3o_obs_dim(c->task);
     if (c->task == 0) {
       double o[24], r;
       int term, trunc;
@@ -120,6 +131,36 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
         env_reset(m, c, e, obs ? obs + 24 * (size_t)i : 0);
       } else if (obs) {
         memcpy(obs + 24 * (size_t)i, o, sizeof(o));
+      }
+      continue;
+    }
+    if (c->task >= 4) {
+      /* ur3e-v0 (ur3e_env.py:139-170), imitation indirect (imitation_env_indirect.py:73-106) and
+         direct (imitation_env_direct.py:74-108): truncation tests t before the increment */
+      if (c->task == 6) {
+        for (int k = 0; k < m->nu; k++) ctrl[k] = a[k];
+      } else {
+        double traj[7] = {a[0], a[1], a[2], -1.209, -1.209, 1.209, a[3]};
+        ur3o_pid_task_ctrl(m, d, traj, &tg, ctrl);
+      }
+      for (int k = 0; k < m->nu; k++) d->ctrl[k] = ctrl[k];
+      for (int s = 0; s < c->frame_skip; s++) ur3o_step(m, d);
+      double o[24];
+      task_obs(m, d, c->task, o);
+      double r = c->task == 4 ? ur3o_reward_v0(m, d, o, a) : -1.0;
+      int term = c->task == 4 ? ur3o_termination_v0(m, d, o) : 0;
+      int trunc = c->max_episode_steps > 0 && e->t >= c->max_episode_steps;
+      e->t += 1;
+      e->ep_return += r;
+      e->ep_len += 1;
+      if (reward) reward[i] = r;
+      if (terminated) terminated[i] = (unsigned char)term;
+      if (truncated) truncated[i] = (unsigned char)trunc;
+      if ((term || trunc) && c->auto_reset) {
+        if (terminal_obs) memcpy(terminal_obs + (size_t)od * i, o, sizeof(double) * od);
+        env_reset(m, c, e, obs ? obs + (size_t)od * i : 0);
+      } else if (obs) {
+        memcpy(obs + (size_t)od * i, o, sizeof(double) * od);
       }
       continue;
     }
@@ -185,6 +226,19 @@ void ur3o_forward_state(const ur3e_model_t* m, const double* qpos, const double*
     for (int i = 0; i < m->nv; i++)
       for (int j = 0; j < m->nv; j++) qM[i * m->nv + j] = d->qM[i][j];
   if (ncon) *ncon = d->ncon;
+  free(d);
+}
+
+/* ur3e-v0 epilogue on a synthetic contact list (golden tests of ur3e_env.py compute_reward /
+   _check_termination and gym_utils.get_table_collision): out_r = reward, out_i = {term, table} */
+void ur3o_v0_epilogue(const ur3e_model_t* m, int ncon, const int* geom1, const int* geom2, const double* obs13,
+                      const double* act4, double* out_r, int* out_i) {
+  ur3o_data* d = (ur3o_data*)calloc(1, sizeof(ur3o_data));
+  d->ncon = ncon;
+  for (int k = 0; k < ncon; k++) { d->contact[k].geom1 = geom1[k]; d->contact[k].geom2 = geom2[k]; }
+  *out_r = ur3o_reward_v0(m, d, obs13, act4);
+  out_i[0] = ur3o_termination_v0(m, d, obs13);
+  out_i[1] = ur3o_table_collision(m, d);
   free(d);
 }
 

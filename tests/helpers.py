@@ -17,14 +17,17 @@ def oracle_config(po, c):
 
 
 class OracleStepper:
-    def __init__(self, n, seed=0, env_id_offset=0, max_episode_steps=2500, model="main"):
+    def __init__(self, n, seed=0, env_id_offset=0, max_episode_steps=2500, model="main",
+                 env_id="gymnasium_env/ur3e-v2"):
         import torch
         from oracle import pyoracle as po
         from ur3e_amd import runtime as rt
         self.torch = torch
+        from ur3e_amd.envs.specs import spec
+        s = spec(env_id)
         md, mc = rt.load_model(model)
-        cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=max_episode_steps, model=md,
-                             seed=seed, env_id_offset=env_id_offset)
+        cfg = rt.make_config(task=s["task"], frame_skip=s["frame_skip"], max_episode_steps=max_episode_steps,
+                             model=md, seed=seed, env_id_offset=env_id_offset, task_gains=s["gains"])
         self.cfg = cfg
         self.ob = po.OracleBatch(mc, oracle_config(po, cfg), n)
         self.n = n

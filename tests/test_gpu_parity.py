@@ -29,30 +29,37 @@ def _oracle_cfg(po, c):
     return oc
 
 
-def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1, tier_con_cap=0):
+def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1, tier_con_cap=0,
+              task_gains=None, max_episode_steps=2500):
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model(model_name)
     cfg = rt.make_config(task=task, frame_skip=frame_skip, model=md, seed=seed, envs_per_block=epb,
-                         tier_con_cap=tier_con_cap,
+                         tier_con_cap=tier_con_cap, task_gains=task_gains, max_episode_steps=max_episode_steps,
                          reset_noise=(model_name == "main"),
                          reset_key=md["id_key_down"] if md["id_key_down"] >= 0 else -1)
     gb = rt.Batch(mc, cfg, n)
     ob = po.OracleBatch(mc, _oracle_cfg(po, cfg), n)
     gobs = gb.obs.cpu().numpy()
-    if task == rt.TASK_GYM_V2:
+    gym = task == rt.TASK_GYM_V2 or task >= rt.TASK_GYM_V0
+    assert gb.obs_dim == ob.od
+    if gym:
         np.testing.assert_array_equal(gobs, ob.obs)
     rng = np.random.default_rng(seed)
     max_dq = 0.0
     max_touch = [0.0]
+    n_done = 0
     for s in range(steps):
         a = action_fn(rng, n, md)
         o_obs, o_rew, o_term, o_trunc, o_tobs = ob.step(a)
         g_obs, g_rew, g_term, g_trunc, g_tobs = gb.step(torch.from_numpy(a))
         if s % check_every == 0 or s == steps - 1:
             torch.cuda.synchronize()
-            if task == rt.TASK_GYM_V2:
+            n_done += int(((o_term > 0) | (o_trunc > 0)).sum())
+            if gym:
+                np.testing.assert_array_equal(g_tobs.cpu().numpy()[o_term | o_trunc > 0],
+                                              o_tobs[o_term | o_trunc > 0], err_msg=f"terminal obs step {s}")
                 np.testing.assert_array_equal(g_rew.cpu().numpy(), o_rew, err_msg=f"reward step {s}")
                 np.testing.assert_array_equal(g_term.cpu().numpy(), o_term, err_msg=f"terminated step {s}")
                 np.testing.assert_array_equal(g_trunc.cpu().numpy(), o_trunc, err_msg=f"truncated step {s}")
@@ -72,6 +79,7 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
                 max_touch[0] = max(max_touch[0], float(ot.max()))
     assert max_dq <= 1e-5
     gb.ovf = gb.overflow_count()
+    gb.n_done = n_done
     gb.max_touch = max_touch[0]
     gb.close()
     return gb
@@ -128,6 +136,41 @@ def test_ctrl_raw():
     def act(rng, n, md):
         return rng.uniform(-20, 20, size=(n, 6))
     _run_pair("ur3e_raw", 3, 32, 100, act, frame_skip=1)
+
+
+def _v0_actions(rng, n, md):
+    # ur3e_env.py:61-66 action Box ([x, y, z] around the mug + gripper)
+    lo = np.array([0.28799994, 0.13349916, 0.005, 0.0])
+    hi = np.array([0.35799994, 0.35349916, 0.165, 1.0])
+    return rng.uniform(lo, hi, size=(n, 4))
+
+
+def test_gym_v0_random_actions():
+    """ur3e-v0 (task 4): 13-d obs, reward with self/table-collision terms, termination, truncation
+    before the increment (T=40 here so auto-reset with the 13-d terminal observation runs)."""
+    from ur3e_amd import runtime as rt
+    gb = _run_pair("main", rt.TASK_GYM_V0, 64, 90, _v0_actions, task_gains=rt.GAINS_V0,
+                   max_episode_steps=40, seed=5)
+    assert gb.n_done > 0
+
+
+def test_imitation_indirect():
+    """imitation-indirect (task 5): v2 action Box through pid_task_ctrl, 24-d obs, reward -1."""
+    from ur3e_amd import runtime as rt
+    gb = _run_pair("main", rt.TASK_IMIT_INDIRECT, 64, 60, _gym_actions, frame_skip=1, max_episode_steps=25,
+                   seed=9)
+    assert gb.n_done > 0
+
+
+def test_imitation_direct():
+    """imitation-direct (task 6): raw ctrl inside actuator ctrlrange, 13-d obs, reward -1."""
+    from ur3e_amd import runtime as rt
+
+    def act(rng, n, md):
+        cr = np.array(md["act_ctrlrange"])
+        return rng.uniform(cr[:, 0], cr[:, 1], size=(n, cr.shape[0]))
+    gb = _run_pair("main", rt.TASK_IMIT_DIRECT, 64, 60, act, max_episode_steps=25, seed=13)
+    assert gb.n_done > 0
 
 
 @pytest.mark.slow

@@ -3,6 +3,7 @@ golden vectors from the reference run on synthetic contact lists."""
 import ctypes
 
 import numpy as np
+import pytest
 
 from oracle import pyoracle as po
 
@@ -33,3 +34,15 @@ def test_predicates(golden, main_model):
         assert out[2] == golden["pred_selfcol"][i], i
         assert out[3] == golden["pred_toppled"][i], i
         assert out[4] == golden["pred_term"][i], i
+
+
+def test_v0_epilogue(golden, main_model):
+    """ur3e-v0 (gymnasium_env/envs/ur3e_env.py) compute_reward, _check_termination and
+    gym_utils.get_table_collision: oracle vs the reference on synthetic contact lists."""
+    md, mc = main_model
+    for o, a, r, te, tb, pl, nc in zip(golden["v0_obs"], golden["v0_act"], golden["v0_rew"], golden["v0_term"],
+                                      golden["v0_table"], golden["v0_pairs"], golden["v0_ncon"]):
+        rr, tt, tab = po.v0_epilogue(mc, pl[:nc], o, a)
+        assert rr == pytest.approx(r, rel=1e-12, abs=1e-9)
+        assert tt == te
+        assert tab == tb

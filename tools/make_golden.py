@@ -77,6 +77,7 @@ import controller.move_j as mvj  # noqa: E402
 import controller.move_l as mvl  # noqa: E402
 import utils.gym_utils as gu  # noqa: E402
 from gymnasium_env.envs.ur3e_env2 import UR3eEnv2  # noqa: E402
+from gymnasium_env.envs.ur3e_env import UR3eEnv  # noqa: E402
 import yaml  # noqa: E402
 
 with open("controller/config/config_l_mug.yml") as f:
@@ -340,6 +341,57 @@ def main():
     out["pred_tcp"] = np.array(ptcp)
     out["pred_hnd"] = np.array(phnd)
     out["pred_obs"] = np.array(pobs)
+
+    # ---- H. UR3eEnv (ur3e-v0) epilogue: compute_reward, _check_termination, get_table_collision
+    #      on synthetic 13-d observations, actions in the v0 Box and contact lists
+    lo0 = np.array([0.28799994, 0.13349916, 0.005, 0.0])
+    hi0 = np.array([0.35799994, 0.35349916, 0.165, 1.0])
+    table_g = md["geom_names"].index("table")
+    arm_g = [md["geom_names"].index(n) for n in ("upperarm", "forearm", "wrist1", "wrist2", "wrist3", "collision")]
+    N0 = 300
+    v0_obs, v0_act, v0_rew, v0_term, v0_tab, v0_pairs, v0_ncon = [], [], [], [], [], [], []
+    for k in range(N0):
+        d = FakeData(md["nsite"], md["nbody"], md["nv"], md["nq"])
+        nc = int(rng.integers(0, 8))
+        pairs = []
+        for _ in range(nc):
+            u = rng.uniform()
+            if u < 0.4:
+                pairs.append((int(rng.choice(pad_g)), fish_g))
+            elif u < 0.55:
+                pairs.append((table_g, int(rng.choice(pad_g + arm_g))))
+            elif u < 0.65:
+                pairs.append((int(rng.choice(arm_g)), int(rng.choice(arm_g))))
+            else:
+                pairs.append((int(rng.integers(0, ng)), int(rng.integers(0, ng))))
+        d.contact = [_Obj(geom1=a, geom2=b) for a, b in pairs]
+        d.ncon = nc
+        mug = rng.uniform([0.25, 0.05, 0.0], [0.36, 0.3, 0.2])
+        if k % 7 == 0:
+            mug = np.array([0.29799994, 0.25, 0.055111]) + rng.normal(size=3) * 0.003
+        d.site_xpos[hnd] = mug
+        g = mug + rng.normal(size=3) * (0.01 if k % 3 else 0.08)
+        if k % 11 == 0:
+            g = mug + np.array([1.2, 0.0, 0.0])
+        if k % 4 == 0:  # gripper >= 0.5 above the block: the cubic height penalty vanishes
+            g[2] = mug[2] + 0.5 + abs(rng.normal()) * 0.01
+        d.site_xpos[tcp] = g
+        pad = g + rng.normal(size=3) * 0.02
+        obs = np.hstack([g, mug, [0.29799994, 0.25, 0.055111], [gu.get_block_grasp_state(fm, d)], pad])
+        a = rng.uniform(lo0, hi0)
+        fake_env = _Obj(model=fm, data=d, collision_cache=cache, t=k)
+        with contextlib.redirect_stdout(io.StringIO()):
+            v0_rew.append(UR3eEnv.compute_reward(fake_env, obs, a))
+            v0_term.append(int(UR3eEnv._check_termination(fake_env, obs)))
+        v0_tab.append(int(gu.get_table_collision(fm, d, cache)))
+        pl = np.zeros((8, 2), int)
+        if nc:
+            pl[:nc] = pairs
+        v0_pairs.append(pl); v0_ncon.append(nc)
+        v0_obs.append(obs); v0_act.append(a)
+    out["v0_obs"], out["v0_act"], out["v0_rew"] = np.array(v0_obs), np.array(v0_act), np.array(v0_rew)
+    out["v0_term"], out["v0_table"] = np.array(v0_term), np.array(v0_tab)
+    out["v0_pairs"], out["v0_ncon"] = np.array(v0_pairs), np.array(v0_ncon)
 
     os.makedirs(OUT, exist_ok=True)
     np.savez_compressed(os.path.join(OUT, "reference_golden.npz"), **out)

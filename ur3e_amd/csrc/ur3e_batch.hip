@@ -586,6 +586,131 @@ KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
   return 0;
 }
 
+/* gym_utils.get_self_collision / get_table_collision (gym_utils.py:146-197) on the LDS contact list */
+template <class KS>
+KD int w_self_collision(KModel m, const KS& s) {
+  for (int ci = 0; ci < s.ncon; ci++) {
+    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    int a1 = (m->mask_arm_bodies >> b1) & 1, a2 = (m->mask_arm_bodies >> b2) & 1;
+    if (a1 && a2) {
+      int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+      if (g1 && g2) continue;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+template <class KS>
+KD int w_table_collision(KModel m, const KS& s) {
+  for (int ci = 0; ci < s.ncon; ci++) {
+    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+    if ((g1 && b2 == m->id_body_table) || (g2 && b1 == m->id_body_table)) return 1;
+  }
+  return 0;
+}
+
+template <class KS>
+KD int w_block_grasp_state(KModel m, const KS& s) {
+  int lp = 0, rp = 0;
+  for (int ci = 0; ci < s.ncon; ci++) {
+    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    if (!(b1 == m->id_body_fish || b2 == m->id_body_fish)) continue;
+    if (b1 == m->id_body_lpad || b2 == m->id_body_lpad) lp = 1;
+    if (b1 == m->id_body_rpad || b2 == m->id_body_rpad) rp = 1;
+  }
+  return lp + rp;
+}
+
+/* UR3eEnv._get_obs (ur3e_env.py) / ImitationEnvDirect._get_obs (imitation_env_direct.py): 13-d */
+template <class KS>
+KD void w_obs13(KModel m, const KS& s, int direct, double obs[13]) {
+  const double* tcp = s.site_xpos[m->id_site_tcp];
+  const double* mug = s.site_xpos[m->id_site_handle];
+  const double* gh = s.xpos[m->id_body_ghost];
+  double tail[3];
+  if (direct) {
+    double vt[6];
+    w_site_velocity(m, s, m->id_site_tcp, vt);
+    tail[0] = vt[3]; tail[1] = vt[4]; tail[2] = vt[5];
+  } else {
+    const double* pad = s.site_xpos[m->id_site_rpad];
+    tail[0] = pad[0]; tail[1] = pad[1]; tail[2] = pad[2];
+  }
+  for (int k = 0; k < 3; k++) { obs[k] = tcp[k]; obs[3 + k] = mug[k]; obs[6 + k] = gh[k]; obs[10 + k] = tail[k]; }
+  obs[9] = (double)w_block_grasp_state(m, s);
+}
+
+KD double k_sq(double x) { return x * x; }
+
+/* UR3eEnv.compute_reward (ur3e_env.py), same expressions as oracle ur3o_reward_v0 */
+KD double k_reward_v0(KModel m, const double obs[13], const double act[4], int selfcol, int tablecol) {
+  const double* gripper_pos = obs;
+  const double* block_center = obs + 3;
+  const double* target_pos = obs + 6;
+  double grasp_state = obs[9];
+  const double* pad_pos = obs + 10;
+  double block_half_height = m->fish_half_z;
+  double block_top_z = block_center[2] + block_half_height;
+  double block_bottom_z = block_center[2] - block_half_height;
+  double pad_to_block_top = pad_pos[2] - block_top_z;
+  double gripper_to_block_center = gripper_pos[2] - block_center[2];
+  double hx = gripper_pos[0] - block_center[0], hy = gripper_pos[1] - block_center[1];
+  double horizontal_error = sqrt(hx * hx + hy * hy);
+  int valid_grasp = grasp_state == 2 && fabs(pad_to_block_top) < 0.04 && horizontal_error < 0.03;
+  double ideal_height_above = 0.5;
+  double height_error = gripper_to_block_center - ideal_height_above;
+  double z_tol = 0.1;
+  double descent_reward = 1 * ((1 / z_tol) * (height_error + z_tol) * ur3e_exp(-(1 / z_tol) * height_error));
+  double grasp_readiness = ur3e_exp(-k_sq(horizontal_error)) * ur3e_exp(-k_sq(pad_to_block_top)) *
+                           ur3e_exp(-k_sq(height_error)) * 100 * ur3e_exp(-k_sq(act[3]));
+  double alignment_reward = 4 * ur3e_exp(-60 * k_sq(horizontal_error));
+  double grip_strength = act[3];
+  double g2 = grasp_state == 2 ? 1.0 : 0.0, g1 = grasp_state >= 1 ? 1.0 : 0.0;
+  double grasp_reward = 5.5 * g1 + 8.5 * g2 + 23.5 * grip_strength * grasp_readiness + 28.5 * g2 * grasp_readiness +
+                        11.5 * g2 * grasp_readiness * ur3e_tanh(8 * grip_strength);
+  double lift_reward = 12 * g2 * ur3e_tanh(4 * block_bottom_z);
+  double px = block_center[0] - target_pos[0], py = block_center[1] - target_pos[1],
+         pz = block_center[2] - target_pos[2];
+  double d_place = sqrt(px * px + py * py + pz * pz);
+  double placement_reward = -2 * d_place + 20 * ur3e_exp(-70 * k_sq(d_place));
+  if (d_place < 0.05 && valid_grasp) placement_reward += 40;
+  double hh = block_center[2] - gripper_pos[2] + 0.5;
+  double dh = -100000000000.0 * (hh * hh * hh);
+  double dangerous_height_penalty = dh < 0 ? dh : 0;
+  double p2b = pad_to_block_top > 0 ? pad_to_block_top : 0;
+  double penalties = -40 * selfcol + -25 * tablecol + -8 * (block_center[2] <= m->fish_topple_z) + -4 * p2b +
+                     dangerous_height_penalty;
+  double action_reward = 700.5 * grip_strength * grasp_readiness;
+  double contact_achievement_bonus = 1700.5 * g2 * grasp_readiness * ur3e_tanh(10 * grip_strength);
+  return descent_reward + alignment_reward + grasp_reward + lift_reward + placement_reward + action_reward +
+         contact_achievement_bonus + penalties;
+}
+
+KD int k_termination_v0(KModel m, const double obs[13], int selfcol) {
+  double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
+  double ex = obs[3] - obs[6], ey = obs[4] - obs[7], ez = obs[5] - obs[8];
+  double d_pick = sqrt(dx * dx + dy * dy + dz * dz);
+  double d_place = sqrt(ex * ex + ey * ey + ez * ez);
+  if (d_place < 0.005) return 1;
+  if (1 < d_pick) return 1;
+  if (selfcol) return 1;
+  if (obs[5] <= m->fish_topple_z) return 1;
+  return 0;
+}
+
+KD int k_is_gym(int task) { return task == UR3E_TASK_GYM_V2 || task >= UR3E_TASK_GYM_V0; }
+__host__ __device__ static inline int k_obs_dim(int task) { return (task == UR3E_TASK_GYM_V0 || task == UR3E_TASK_IMIT_DIRECT) ? 13 : 24; }
+
+/* the task's observation into obs (lane 0) */
+template <class KS>
+KD void w_task_obs(KModel m, const KS& s, int task, double* obs) {
+  if (task == UR3E_TASK_GYM_V0) w_obs13(m, s, 0, obs);
+  else if (task == UR3E_TASK_IMIT_DIRECT) w_obs13(m, s, 1, obs);
+  else w_obs_v2(m, s, obs);
+}
+
 /* per-env step results staged in LDS; nothing reaches global memory before w_commit, so a
    compact-tier env that overflows (s.ovf) can be recomputed from its untouched state */
 struct WOut {
@@ -621,21 +746,22 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
   for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
+  const int od = k_obs_dim(c.task);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
-    if (stepped && c.task == UR3E_TASK_GYM_V2) {
+    if (stepped && k_is_gym(c.task)) {
       if (rew_out) rew_out[e] = o.r;
       if (term_out) term_out[e] = (unsigned char)o.term;
       if (trunc_out) trunc_out[e] = (unsigned char)o.trunc;
     }
   }
-  if (c.task == UR3E_TASK_GYM_V2) {
+  if (k_is_gym(c.task)) {
     if (stepped && o.did_reset && tobs_out)
-      for (int k = tid; k < 24; k += NT) tobs_out[(size_t)e * 24 + k] = o.tobs[k];
+      for (int k = tid; k < od; k += NT) tobs_out[(size_t)e * od + k] = o.tobs[k];
   }
-  if (obs_out && (c.task == UR3E_TASK_GYM_V2 || c.obs_sites))
-    for (int k = tid; k < 24; k += NT) obs_out[(size_t)e * 24 + k] = o.obs[k];
+  if (obs_out && (k_is_gym(c.task) || c.obs_sites))
+    for (int k = tid; k < od; k += NT) obs_out[(size_t)e * od + k] = o.obs[k];
 }
 
 /* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
@@ -669,7 +795,7 @@ WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
 template <int NT, class KS>
 WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c, KS& s, WOut& o) {
   const int tid = threadIdx.x;
-  if (tid == 0 && (c.task == UR3E_TASK_GYM_V2 || c.obs_sites)) w_obs_v2(m, s, o.obs);
+  if (tid == 0 && (k_is_gym(c.task) || c.obs_sites)) w_task_obs(m, s, c.task, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
 }
@@ -693,9 +819,10 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
   SYNC();
   if (tid == 0) {
     double ctrl[K_NU];
-    if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
+    if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L || c.task == UR3E_TASK_GYM_V0 ||
+        c.task == UR3E_TASK_IMIT_INDIRECT) {
       double traj[7];
-      if (c.task == UR3E_TASK_GYM_V2) {
+      if (c.task != UR3E_TASK_TRAJ_L) { /* [x, y, z] + fixed rotvec + grip */
         traj[0] = o.a[0]; traj[1] = o.a[1]; traj[2] = o.a[2];
         traj[3] = -1.209; traj[4] = -1.209; traj[5] = 1.209;
         traj[6] = o.a[3];
@@ -726,7 +853,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     for (int k = 0; k < m->nu; k++) s.ctrl[k] = ctrl[k];
   }
   SYNC();
-  const int fs = (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  const int fs = (k_is_gym(c.task) || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
   /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
   int sub = 0, retried = 0, resetting = 0;
   w_step_pre<NT>(m, s);
@@ -749,7 +876,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     }
     w_make_carry<NT>(m, pl, s, o.carry);
     SYNC();
-    if (c.task != UR3E_TASK_GYM_V2) {
+    if (!k_is_gym(c.task)) {
       if (tid == 0) {
         o.t += 1; o.ep_len += 1;
         if (c.obs_sites) w_obs_v2(m, s, o.obs);
@@ -757,7 +884,25 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       SYNC();
       return true;
     }
-    if (tid == 0) {
+    if (tid == 0 && c.task != UR3E_TASK_GYM_V2) {
+      /* ur3e-v0 / imitation envs: truncation tests t before the increment (ur3e_env.py:152-163,
+         imitation_env_indirect.py:96-101, imitation_env_direct.py:98-103) */
+      w_task_obs(m, s, c.task, o.obs);
+      double r = -1.0;
+      int term = 0;
+      if (c.task == UR3E_TASK_GYM_V0) {
+        const int sc = w_self_collision(m, s);
+        r = k_reward_v0(m, o.obs, o.a, sc, w_table_collision(m, s));
+        term = k_termination_v0(m, o.obs, sc);
+      }
+      const int trunc = c.max_episode_steps > 0 && o.t >= c.max_episode_steps;
+      o.t += 1;
+      o.ep_return += r;
+      o.ep_len += 1;
+      o.r = r;
+      o.term = term;
+      o.trunc = trunc;
+    } else if (tid == 0) {
       int t = o.t + 1;
       o.t = t;
       w_obs_v2(m, s, o.obs);
@@ -777,7 +922,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     }
     SYNC();
     if ((o.term || o.trunc) && c.auto_reset) {
-      for (int k = tid; k < 24; k += NT) o.tobs[k] = o.obs[k];
+      for (int k = tid; k < k_obs_dim(c.task); k += NT) o.tobs[k] = o.obs[k];
       if (tid == 0) o.did_reset = 1;
       SYNC();
       w_reset_prep<NT>(m, c, e, s, o);
@@ -1005,7 +1150,13 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   if (!model || !cfg || !out || n_envs <= 0) return fail(UR3E_EINVAL, "null argument or n_envs <= 0");
   int rc = check_model(model);
   if (rc) return rc;
-  if (cfg->task < 0 || cfg->task > 3) return fail(UR3E_EINVAL, "unknown task");
+  if (cfg->task < 0 || cfg->task > 6) return fail(UR3E_EINVAL, "unknown task");
+  if (cfg->task >= UR3E_TASK_GYM_V0 && cfg->envs_per_block > 0)
+    return fail(UR3E_EINVAL, "ur3e-v0 / imitation tasks need a workgroup-per-env layout (envs_per_block <= 0)");
+  if (cfg->task >= UR3E_TASK_GYM_V0 && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
+                                        model->id_body_ghost < 0 || model->id_body_fish < 0 ||
+                                        model->id_site_rpad < 0))
+    return fail(UR3E_EMODEL, "ur3e-v0 / imitation tasks need assets/main.xml");
   if (cfg->task == UR3E_TASK_GYM_V2 && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
                                         model->id_body_ghost < 0 || model->id_body_fish < 0))
     return fail(UR3E_EMODEL, "gym ur3e-v2 task needs tcp/handle_site/ghost/fish (assets/main.xml)");
@@ -1119,7 +1270,9 @@ extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* 
 extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adim, double* d_obs, double* d_reward,
                                uint8_t* d_terminated, uint8_t* d_truncated, double* d_terminal_obs, void* stream) {
   if (!b || !d_actions) return fail(UR3E_EINVAL, "null handle or actions");
-  int need = b->cfg.task == UR3E_TASK_GYM_V2 ? 4 : (b->cfg.task == UR3E_TASK_CTRL ? b->host_model.nu : 7);
+  const int task = b->cfg.task;
+  int need = (task == UR3E_TASK_GYM_V2 || task == UR3E_TASK_GYM_V0 || task == UR3E_TASK_IMIT_INDIRECT) ? 4
+             : (task == UR3E_TASK_CTRL || task == UR3E_TASK_IMIT_DIRECT) ? b->host_model.nu : 7;
   if (adim != need) return fail(UR3E_EINVAL, "action dimension mismatch for task (expected " + std::to_string(need) + ")");
   HIPCHK(hipSetDevice(b->device));
   hipStream_t st = (hipStream_t)stream;
@@ -1292,6 +1445,8 @@ extern "C" int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* to
   HIPCHK(hipMemcpy(total, b->d_ovf_total, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return UR3E_OK;
 }
+
+extern "C" int ur3e_batch_obs_dim(const ur3e_batch_t* b) { return b ? k_obs_dim(b->cfg.task) : 0; }
 
 extern "C" int ur3e_batch_num_envs(const ur3e_batch_t* b) { return b ? b->n : 0; }
 extern "C" int ur3e_batch_nq(const ur3e_batch_t* b) { return b ? b->host_model.nq : 0; }

@@ -19,7 +19,7 @@ import time
 import numpy as np
 
 from .spaces import Box
-from .ur3e_env2 import UR3E_V2_ACTION_HIGH, UR3E_V2_ACTION_LOW
+from .specs import spec
 
 try:  # subclass SB3's VecEnv when it is installed (it is not in this image)
     from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _SB3VecEnv
@@ -29,16 +29,21 @@ except Exception:  # pragma: no cover
 
 class UR3eVecEnv(_SB3VecEnv):
     def __init__(self, num_envs: int = 4096, device: int = 0, seed: int = 0, stepper=None, env_id_offset: int = 0,
-                 envs_per_block: int = 0, max_episode_steps: int = 2500):
+                 envs_per_block: int = 0, max_episode_steps: int | None = None,
+                 env_id: str = "gymnasium_env/ur3e-v2"):
+        s = spec(env_id)
+        self.env_id = env_id
         self.num_envs = num_envs
-        self.observation_space = Box(low=-np.inf, high=np.inf, shape=(24,), dtype=np.float64)
-        self.action_space = Box(low=UR3E_V2_ACTION_LOW, high=UR3E_V2_ACTION_HIGH, dtype=np.float64)
+        self.observation_space = Box(low=-np.inf, high=np.inf, shape=(s["obs_dim"],), dtype=np.float64)
+        self.action_space = Box(low=s["low"], high=s["high"], dtype=np.float64)
         self.render_mode = None
         if stepper is None:
             from .. import runtime as rt
             md, mc = rt.load_model("main")
-            cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=max_episode_steps,
-                                 model=md, seed=seed, env_id_offset=env_id_offset, envs_per_block=envs_per_block)
+            T = s["T"] if max_episode_steps is None else max_episode_steps
+            cfg = rt.make_config(task=s["task"], frame_skip=s["frame_skip"], max_episode_steps=T,
+                                 model=md, seed=seed, env_id_offset=env_id_offset, envs_per_block=envs_per_block,
+                                 task_gains=s["gains"])
             stepper = rt.Batch(mc, cfg, num_envs, device=device)
         self.stepper = stepper
         self._actions = None
@@ -84,7 +89,7 @@ class UR3eVecEnv(_SB3VecEnv):
         import torch
         a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, dtype=np.float64))
         # no clipping here: like UR3eEnv2.step, actions are used as given (SB3 clips to the Box itself)
-        return self.stepper.step(a.reshape(self.num_envs, 4).to(torch.float64))
+        return self.stepper.step(a.reshape(self.num_envs, self.action_space.shape[0]).to(torch.float64))
 
     def close(self):
         if hasattr(self.stepper, "close"):

@@ -37,7 +37,7 @@ from .surrogate import DENSITY, MESH_SURROGATE
 MAXBODY, MAXJNT, MAXNQ, MAXNV = 28, 16, 24, 24
 MAXGEOM, MAXSITE, MAXCPAIR, MAXEQ = 32, 20, 320, 4
 MAXU, MAXTEN, MAXTENWRAP, MAXKEY, MAXTOUCH = 8, 2, 4, 2, 4
-MODEL_VERSION = 3
+MODEL_VERSION = 4
 
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = 0, 1, 2, 3
 GEOM_PLANE, GEOM_BOX = 0, 6
@@ -583,6 +583,7 @@ def compile_mjcf(path: str) -> dict:
     m["id_body_ghost"] = _nid("body", "ghost")
     m["id_body_lpad"] = _nid("body", "left_pad")
     m["id_body_rpad"] = _nid("body", "right_pad")
+    m["id_body_table"] = _nid("body", "table")
     m["id_key_home"] = key_names.index("home") if "home" in key_names else -1
     m["id_key_down"] = key_names.index("down") if "down" in key_names else -1
 
@@ -606,8 +607,10 @@ def compile_mjcf(path: str) -> dict:
     if fish >= 0:
         fg = [g for g in geoms if g["body"] == fish][0]
         m["fish_topple_z"] = max(fg["size"][0], fg["size"][1])
+        m["fish_half_z"] = fg["size"][2]  # get_body_size(m, "fish")[-1] (ur3e_env.py compute_reward)
     else:
         m["fish_topple_z"] = 0.0
+        m["fish_half_z"] = 0.0
 
     _set_const(m)
     return m
@@ -904,6 +907,8 @@ class UR3eModelC(ctypes.Structure):
         ("id_key_home", _i), ("id_key_down", _i),
         ("mask_arm_bodies", ctypes.c_uint), ("mask_gripper_bodies", ctypes.c_uint),
         ("fish_topple_z", _d),
+        ("id_body_table", _i),
+        ("fish_half_z", _d),
     ]
 
 

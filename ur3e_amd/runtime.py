@@ -23,10 +23,14 @@ LIB_PATH = os.environ.get("UR3E_LIB", os.path.join(_HERE, "_lib", "libur3e_amd.s
 ASSETS = os.path.join(_HERE, "assets")
 
 TASK_GYM_V2, TASK_TRAJ_L, TASK_MOVE_J, TASK_CTRL = 0, 1, 2, 3
+TASK_GYM_V0, TASK_IMIT_INDIRECT, TASK_IMIT_DIRECT = 4, 5, 6
 
 # controller/config/config_l_mug.yml (used by UR3eEnv2, ur3e_env2.py:66-68)
 GAINS_L_MUG = dict(kp_pos=[220.0, 220.0, 120.0], kd_pos=[20.0, 20.0, 40.0],
                    kp_rot=[35.0, 15.0, 15.0], kd_rot=[2.0, 2.0, 2.0])
+# gymnasium_env/envs/ur3e_env.py:49-55 (UR3eEnv, ur3e-v0)
+GAINS_V0 = dict(kp_pos=[320.0, 320.0, 320.0], kd_pos=[20.0, 20.0, 25.0],
+                kp_rot=[325.0, 325.0, 325.0], kd_rot=[2.0, 2.0, 2.0])
 # controller/config/config_j.yml (move_j)
 GAINS_J = dict(kp=[20.0, 380.0, 300.0, 20.0, 30.0, 10.0], kd=[5.0] * 6)
 
@@ -64,7 +68,7 @@ def load_library():
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
-    for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu"):
+    for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim"):
         getattr(L, f).argtypes = [vp]
     _lib = L
     del dp
@@ -133,11 +137,12 @@ class Batch:
         _check(self.L.ur3e_batch_create(ctypes.byref(model_c), ctypes.byref(cfg), n_envs, device, ctypes.byref(h)))
         self.h = h
         f64 = dict(dtype=torch.float64, device=self.device)
-        self.obs = torch.zeros((n_envs, 24), **f64)
+        self.obs_dim = self.L.ur3e_batch_obs_dim(h)
+        self.obs = torch.zeros((n_envs, self.obs_dim), **f64)
         self.reward = torch.zeros(n_envs, **f64)
         self.terminated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
         self.truncated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
-        self.terminal_obs = torch.zeros((n_envs, 24), **f64)
+        self.terminal_obs = torch.zeros((n_envs, self.obs_dim), **f64)
         self.reset()
 
     def _stream(self):
@@ -226,4 +231,4 @@ class Batch:
 
 
 __all__ = ["Batch", "make_config", "load_model", "load_library", "TASK_GYM_V2", "TASK_TRAJ_L", "TASK_MOVE_J",
-           "TASK_CTRL", "GAINS_L_MUG", "GAINS_J", "np"]
+           "TASK_CTRL", "TASK_GYM_V0", "TASK_IMIT_INDIRECT", "TASK_IMIT_DIRECT", "GAINS_L_MUG", "GAINS_V0", "GAINS_J", "np"]
