@@ -124,6 +124,11 @@ int ur3e_batch_get_carry(ur3e_batch_t* b, double* d_carry, void* stream);
    utils/utils.py:238-240 (get_boolean_grasp_contact) */
 int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream);
 
+/* d.ctrl after the last step, d_ctrl [N, nu]: the controller output the step applied (pid_task_ctrl
+   torques + grip, PD torques, or the raw action); zero after a reset, like mj_resetData.  Replaces the
+   `u` that gymnasium_src/scripts/imitation_rl/collect_demos.py:134-148 records as the direct action */
+int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream);
+
 /* envs the compact tier handed to the full-capacity tier since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 

@@ -96,7 +96,9 @@ class OracleBatch:
         sz = self.L.ur3o_sizeof_env()
         ptr = ctypes.cast(ctypes.addressof(self.buf) + sz * i, ctypes.c_void_p)
         self.L.ur3o_env_diag(ptr, ctypes.byref(ncon), ctypes.byref(nefc), ctypes.byref(nit), _p(touch))
-        return dict(ncon=ncon.value, nefc=nefc.value, niter=nit.value, touch=touch)
+        ctrl = np.zeros(8)
+        self.L.ur3o_env_ctrl(ptr, _p(ctrl))
+        return dict(ncon=ncon.value, nefc=nefc.value, niter=nit.value, touch=touch, ctrl=ctrl)
 
 
 def forward_state(model_c, qpos, qvel=None):

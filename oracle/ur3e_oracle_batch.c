@@ -211,6 +211,11 @@ void ur3o_env_diag(const ur3o_env* e, int* ncon, int* nefc, int* niter, double* 
   for (int k = 0; k < UR3E_MAXTOUCH; k++) touch[k] = e->d.touch[k];
 }
 
+/* d.ctrl applied by the last step (UR3E_MAXU entries) */
+void ur3o_env_ctrl(const ur3o_env* e, double* ctrl) {
+  for (int k = 0; k < UR3E_MAXU; k++) ctrl[k] = e->d.ctrl[k];
+}
+
 /* single-env helpers for golden-vector tests */
 void ur3o_forward_state(const ur3e_model_t* m, const double* qpos, const double* qvel, double* site_xpos,
                         double* site_xmat, double* qfrc_bias, double* qM, int* ncon) {

@@ -28,3 +28,32 @@ def test_pick_place_torch_rows(golden):
     pp = bt.PickPlaceTorch(s, picks, places)
     for t in list(range(0, 7200, 97)) + [7199]:
         np.testing.assert_array_equal(pp.row(t).numpy(), golden["pp_rows"][:, t // 120])
+
+
+def _aug_noise(seed, n=1):
+    # np.random.seed(seed) + the reference's rand(rows, 7) calls == one RandomState stream in C order
+    return np.random.RandomState(seed).random_sample((n, bt.AUG_NOISE_ROWS, 7))
+
+
+def test_augmented_golden(golden):
+    """build_traj_l_pick_place_imitation_augmented (build_traj.py:61-125) with np.random seeded."""
+    idx = golden["aug_idx"]
+    for i in range(len(golden["aug_start"])):
+        rs = np.random.RandomState(int(golden["aug_seed"][i]))
+        block, target = golden["aug_dest"][i]
+        tr = bt.build_traj_l_pick_place_imitation_augmented(golden["aug_start"][i], [block, target], 120,
+                                                            rand=rs.rand)
+        assert tr.shape == (bt.AUG_T, 7)
+        np.testing.assert_array_equal(tr[idx], golden["aug_rows"][i])
+
+
+def test_augmented_torch_batch(golden):
+    """The batched builder reproduces every golden trajectory from the same uniform stream."""
+    idx = golden["aug_idx"]
+    n = len(golden["aug_start"])
+    noise = np.concatenate([_aug_noise(int(s)) for s in golden["aug_seed"]])
+    aug = bt.AugmentedPickPlaceTorch(torch.from_numpy(golden["aug_start"]), torch.from_numpy(golden["aug_dest"][:, 0]),
+                                     torch.from_numpy(golden["aug_dest"][:, 1]), torch.from_numpy(noise))
+    assert aug.traj.shape == (bt.AUG_T, n, 7)
+    for i in range(n):
+        np.testing.assert_array_equal(aug.traj[:, i].numpy()[idx], golden["aug_rows"][i])

@@ -219,3 +219,37 @@ def test_move_l_mug_scripted_pick():
     st = task_space_state(gb)
     assert st.shape == (n, 7)
     drv.close()
+
+
+@pytest.mark.parametrize("mode", ["indirect", "direct"])
+def test_collect_demos_batched(mode):
+    """collect_demos.py:86-189 batched: augmented-trajectory rows through pid_task_ctrl + one mj_step;
+    recorded obs (get_obs) and actions ([x, y, z, u_grip] or the 7 ctrl) are bit-exact vs the oracle
+    stepping the same rows, with down-sampling."""
+    torch = _torch()
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.collect_demos import DemoCollector
+    n, steps, ds = 16, 700, 3
+    col = DemoCollector(n, action_mode=mode, noise_mag="low", down_sample=ds, seed=2)
+    gb = col.batch
+    ob = po.OracleBatch(gb.model_c, _oracle_cfg(po, gb.cfg), n)
+    np.testing.assert_array_equal(col.obs0.cpu().numpy(), ob.obs)
+    rows = col.traj.traj[:steps].cpu().numpy()
+    obs, acts = col.run(steps)
+    obs, acts = obs.cpu().numpy(), acts.cpu().numpy()
+    assert obs.shape == ((steps + ds - 1) // ds + 1, n, 24)
+    j = 0
+    for t in range(steps):
+        o_obs = ob.step(rows[t])[0]
+        if t % ds == 0:
+            ctrl = np.stack([ob.diag(i)["ctrl"][:gb.nu] for i in range(n)])
+            if mode == "indirect":
+                exp = np.concatenate([rows[t][:, :3], ctrl[:, -1:]], axis=1)
+            else:
+                exp = ctrl
+            np.testing.assert_array_equal(acts[j], exp, err_msg=f"acts row {t}")
+            np.testing.assert_array_equal(obs[j + 1], o_obs, err_msg=f"obs row {t}")
+            j += 1
+    trajs = col.trajectories(torch.from_numpy(obs), torch.from_numpy(acts))
+    assert len(trajs) == n and trajs[0].obs.shape[0] == trajs[0].acts.shape[0] + 1
+    col.close()

@@ -393,6 +393,24 @@ def main():
     out["v0_term"], out["v0_table"] = np.array(v0_term), np.array(v0_tab)
     out["v0_pairs"], out["v0_ncon"] = np.array(v0_pairs), np.array(v0_ncon)
 
+    # ---- I. augmented imitation trajectories (collect_demos.py:104-106), global np.random seeded per case
+    aug_start, aug_dest, aug_seed, aug_idx, aug_rows = [], [], [], None, []
+    for k, seed in enumerate([3, 1234]):
+        s = np.array([0.29799994, 0.13349916, 0.1682003, -1.20920499, -1.20920054, 1.20920054, 0.0])
+        s[:3] += rng.normal(size=3) * 0.01
+        pick = np.concatenate([rng.uniform([0.29, 0.0, 0.05], [0.31, 0.14, 0.06]), s[3:6], [0.0]])
+        place = np.concatenate([[0.29799994, 0.25, 0.055111], s[3:6], [1.0]])
+        np.random.seed(seed)
+        tr = bt.build_traj_l_pick_place_imitation_augmented(s.copy(), [pick.copy(), place.copy()], 120)
+        assert tr.shape == (10500, 7)
+        idx = sorted(set(range(0, 10500, 10)) | {j * 1500 + 1499 for j in range(7)} |
+                     {j * 1500 + 999 for j in range(7)} | {j * 1500 + 1000 for j in range(7)})
+        aug_idx = np.array(idx)
+        aug_rows.append(tr[aug_idx])
+        aug_start.append(s); aug_dest.append(np.stack([pick, place])); aug_seed.append(seed)
+    out["aug_start"], out["aug_dest"], out["aug_seed"] = np.array(aug_start), np.array(aug_dest), np.array(aug_seed)
+    out["aug_idx"], out["aug_rows"] = aug_idx, np.array(aug_rows)
+
     os.makedirs(OUT, exist_ok=True)
     np.savez_compressed(os.path.join(OUT, "reference_golden.npz"), **out)
     meta = {"generator": "tools/make_golden.py", "reference": "derekc22/UR3e @ /root/reference",

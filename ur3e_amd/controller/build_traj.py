@@ -8,6 +8,12 @@
   reference, `destinations` are not mutated in place.
 * build_traj_j               (build_traj.py:387-470): np.random.seed(42) control
   points + cubic interp1d, 500 samples, held `hold` times, grip 0.
+* build_traj_l_pick_place_imitation_augmented (build_traj.py:61-125): seven
+  15-point segments held 100 rows each (pick at start height / down / grab /
+  up +0.15 / place / descend +0.025 / drop), uniform noise u/40 or u/20 on all
+  but the last 500 rows of each segment (all rows of `up`); each segment starts
+  from the previous segment's last (noisy) row.  `AugmentedPickPlaceTorch` is
+  the batched GPU version used by controller/collect_demos.py.
 
 Also a torch version of pick_place that evaluates rows analytically per env
 and step on the GPU (`PickPlaceTorch`), used by the batched scripted driver
@@ -74,6 +80,109 @@ def build_traj_j(start, hold):
         cols.append(interp1d(t_control, ctrl, kind="cubic")(t))
     g = np.tile([0, 0, 0], num_points // 3 + 1)[:num_points]
     return np.repeat(np.vstack(cols + [g]).T, repeats=hold, axis=0)
+
+
+# build_traj.py:70-73: noise norms; 500-row noiseless buffer at the end of each segment
+AUG_HOLD = 100
+AUG_BUFFER = 500
+AUG_SEG_ROWS = NUM_POINTS * AUG_HOLD                       # 1500
+AUG_T = 7 * AUG_SEG_ROWS                                    # 10500
+# (noise norm, rows with noise) per segment: pick, down, grab, up, place, descend, drop
+AUG_NOISE = [(40, AUG_SEG_ROWS - AUG_BUFFER), (40, AUG_SEG_ROWS - AUG_BUFFER), (20, AUG_SEG_ROWS - AUG_BUFFER),
+             (20, AUG_SEG_ROWS), (20, AUG_SEG_ROWS - AUG_BUFFER), (20, AUG_SEG_ROWS - AUG_BUFFER),
+             (20, AUG_SEG_ROWS - AUG_BUFFER)]
+AUG_NOISE_ROWS = sum(r for _, r in AUG_NOISE)              # 7500 uniform rows of 7 per trajectory
+
+
+def build_traj_l_pick_place_imitation_augmented(start, destinations, hold=None, rand=None):
+    """build_traj.py:61-125 (`hold` is ignored there too: every segment holds 100 rows).
+
+    rand(rows, 7) supplies the uniform noise in the reference's draw order (default: the global
+    np.random.rand, as the reference)."""
+    rand = np.random.rand if rand is None else rand
+    block, target = (np.asarray(x, dtype=np.float64) for x in destinations)
+    start = np.asarray(start, dtype=np.float64)
+
+    def seg(a, b, k):
+        norm, nrows = AUG_NOISE[k]
+        tr = build_traj_l_point_custom(a, b, AUG_HOLD)
+        noise = rand(nrows, 7) / norm
+        if nrows < tr.shape[0]:
+            noise = np.vstack([noise, np.zeros((tr.shape[0] - nrows, 7))])
+        return tr + noise
+
+    pick = np.hstack([block[:2], [start[2]], block[3:]])
+    t_pick = seg(start, pick, 0)
+    down = np.hstack([t_pick[-1, :2], [block[2]], t_pick[-1, 3:]])
+    t_down = seg(t_pick[-1, :], down, 1)
+    grab = np.append(t_down[-1, :-1], 1)
+    t_grab = seg(t_down[-1, :], grab, 2)
+    up = t_grab[-1, :] + [0, 0, 0.15, 0, 0, 0, 0]
+    t_up = seg(t_grab[-1, :], up, 3)
+    place = np.hstack([target[:2], t_up[-1, 2], target[3:]])
+    t_place = seg(t_up[-1, :], place, 4)
+    descend = target + [0, 0, 0.025, 0, 0, 0, 0]
+    t_descend = seg(t_place[-1, :], descend, 5)
+    end_drop = np.append(t_descend[-1, :-1], 0)
+    t_drop = seg(t_descend[-1, :], end_drop, 6)
+    return np.vstack([t_pick, t_down, t_grab, t_up, t_place, t_descend, t_drop])
+
+
+class AugmentedPickPlaceTorch:
+    """build_traj_l_pick_place_imitation_augmented for N trajectories at once, on the device of `starts`.
+
+    starts / blocks / targets: [N, 7] float64.  noise: [N, AUG_NOISE_ROWS, 7] uniform draws in the
+    reference's per-trajectory order (pick, down, grab, up, place, descend, drop), e.g.
+    np.random.rand(N * 7500 * 7) for a seeded reference run, or torch.rand on the GPU.
+    `traj` is the time-major [AUG_T, N, 7] table (2.4 GB at N = 4096: resident in HBM), and
+    traj[:, i] equals the reference's trajectory for (starts[i], [blocks[i], targets[i]]) bit-for-bit.
+    """
+
+    def __init__(self, starts, blocks, targets, noise):
+        import torch
+        dev = starts.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        n = starts.shape[0]
+        tt = torch.from_numpy(np.linspace(0, 1, NUM_POINTS + 1)[1:]).to(dev)
+        noise = noise.to(**f64)
+        assert noise.shape == (n, AUG_NOISE_ROWS, 7)
+        self.T = AUG_T
+        self.traj = torch.empty((AUG_T, n, 7), **f64)
+        off = 0
+
+        def seg(k, a, b):
+            nonlocal off
+            norm, nrows = AUG_NOISE[k]
+            slope = (b - a) / (1.0 - 0.0)
+            pts = slope[None] * (tt[:, None, None] - 0.0) + a[None]      # [15, N, 7]
+            pts[-1] = b                                                  # np.interp hits `stop` exactly
+            rows = pts.repeat_interleave(AUG_HOLD, dim=0)                # [1500, N, 7]
+            nz = torch.zeros_like(rows)
+            nz[:nrows] = noise[:, off:off + nrows].transpose(0, 1) / norm
+            off += nrows
+            out = self.traj[k * AUG_SEG_ROWS:(k + 1) * AUG_SEG_ROWS]
+            torch.add(rows, nz, out=out)
+            return out[-1]
+
+        def col(x, k, v):
+            y = x.clone()
+            y[:, k] = v
+            return y
+
+        e = seg(0, starts, col(blocks, 2, starts[:, 2]))
+        e = seg(1, e, col(e, 2, blocks[:, 2]))
+        e = seg(2, e, col(e, 6, 1.0))
+        dz = torch.tensor([0, 0, 0.15, 0, 0, 0, 0], **f64)
+        e = seg(3, e, e + dz)
+        pl = targets.clone()
+        pl[:, 2] = e[:, 2]
+        e = seg(4, e, pl)
+        dz = torch.tensor([0, 0, 0.025, 0, 0, 0, 0], **f64)
+        e = seg(5, e, targets + dz)
+        seg(6, e, col(e, 6, 0.0))
+
+    def row(self, t: int):
+        return self.traj[t]
 
 
 class PickPlaceTorch:

@@ -297,6 +297,7 @@ struct KState {
   int* ncon;
   int* nwarn;
   double* touch; /* [env][UR3E_MAXTOUCH] touch sensors after the last forward */
+  double* ctrl;  /* [env][UR3E_MAXU] d.ctrl after the last step (the controller output it applied) */
 };
 
 struct KConfig {
@@ -336,6 +337,7 @@ KD void k_store(KModel m, const KState& s, int e, const KData* d, const double* 
   s.ncon[e] = d->ncon;
   s.nwarn[e] = d->nwarn;
   for (int k = 0; k < UR3E_MAXTOUCH; k++) s.touch[(size_t)e * UR3E_MAXTOUCH + k] = d->touch[k];
+  for (int k = 0; k < m->nu; k++) s.ctrl[(size_t)e * UR3E_MAXU + k] = d->ctrl[k];
 }
 
 /* reset one env in registers/scratch: keyframe (+ mug noise), forward, obs, carry */
@@ -746,6 +748,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
   for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
+  for (int k = tid; k < m->nu; k += NT) st.ctrl[(size_t)e * UR3E_MAXU + k] = s.ctrl[k];
   const int od = k_obs_dim(c.task);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
@@ -1046,6 +1049,12 @@ __global__ void k_env_get_touch(KState s, int ntouch, double* __restrict__ out) 
   for (int k = 0; k < ntouch; k++) out[(size_t)e * ntouch + k] = s.touch[(size_t)e * UR3E_MAXTOUCH + k];
 }
 
+__global__ void k_env_get_ctrl(KState s, int nu, double* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  for (int k = 0; k < nu; k++) out[(size_t)e * nu + k] = s.ctrl[(size_t)e * UR3E_MAXU + k];
+}
+
 __global__ void k_env_get_info(KState s, int* ncon, int* ep_len, double* ep_ret, int* nwarn) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= s.n) return;
@@ -1219,6 +1228,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMalloc(&s.nwarn, sizeof(int) * nd));
   HIPCHK(hipMalloc(&s.touch, sizeof(double) * nd * UR3E_MAXTOUCH));
   HIPCHK(hipMemset(s.touch, 0, sizeof(double) * nd * UR3E_MAXTOUCH));
+  HIPCHK(hipMalloc(&s.ctrl, sizeof(double) * nd * UR3E_MAXU));
+  HIPCHK(hipMemset(s.ctrl, 0, sizeof(double) * nd * UR3E_MAXU));
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
@@ -1240,7 +1251,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
   void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
-                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->d_ovf_list, b->d_ovf_count,
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->d_ovf_list, b->d_ovf_count,
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   (void)hipEventDestroy(b->ev0);
@@ -1416,6 +1427,15 @@ extern "C" int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stre
   if (b->host_model.ntouch > 0)
     hipLaunchKernelGGL(k_env_get_touch, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
                        b->host_model.ntouch, d_touch);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream) {
+  if (!b || !d_ctrl) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_get_ctrl, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
+                     b->host_model.nu, d_ctrl);
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }

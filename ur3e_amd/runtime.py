@@ -68,6 +68,7 @@ def load_library():
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
+    L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim"):
         getattr(L, f).argtypes = [vp]
     _lib = L
@@ -196,6 +197,12 @@ class Batch:
         nw = t.empty(self.n, dtype=t.int32, device=self.device)
         _check(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
         return dict(ncon=nc, ep_len=el, ep_return=er, nwarn=nw)
+
+    def get_ctrl(self):
+        """[N, nu] d.ctrl applied by the last step."""
+        out = self.torch.empty((self.n, self.nu), dtype=self.torch.float64, device=self.device)
+        _check(self.L.ur3e_batch_get_ctrl(self.h, _ptr(out), self._stream()))
+        return out
 
     def get_carry(self):
         """[N, 54] stale-kinematics snapshot: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6]."""
