@@ -30,6 +30,9 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # algorithmic HBM bytes per env-step for main.xml (nq 21, nv 20, n_a 4, n_obs 24)
 ALGO_BYTES_PER_ENV_STEP = 1898
+# MI355X vector FP64 (AMD public spec): the path's real bound is FP64 latency at one
+# wavefront per SIMD, so the algorithmic FP64 rate is reported beside the HBM roofline
+FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
 def cpu_baseline(n_envs_sample=4096, steps=200, seed=0):
@@ -164,6 +167,18 @@ def main():
                     prof_traffic = json.load(f).get("hbm_bytes_per_launch")
             except Exception:
                 prof_traffic = None
+        fp64 = None
+        ff = os.path.join(REPO, "profiles", "flops_r01.json")
+        if os.path.exists(ff):
+            try:
+                with open(ff) as f:
+                    fpe = json.load(f)["flops_per_env_step"]
+                ach = fpe * n / (step_kernel_ms * 1e-3) / 1e12
+                fp64 = {"bound": "fp64-vector", "achieved": ach, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / FP64_VECTOR_PEAK_TFLOPS, "flops_per_env_step": fpe,
+                        "source": "profiles/flops_r01.json (tools/count_flops.py: counting build of the oracle)"}
+            except Exception:
+                fp64 = None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -198,6 +213,7 @@ def main():
                          "stream_avg_ms": kernel_avg_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
                          "note": "path is FP64-latency-bound (SURVEY.md §8d); HBM fraction reported as required"},
+            "roofline_fp64": fp64,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -48,8 +48,8 @@ def _p(a):
 class OracleBatch:
     """N independent oracle envs with the same step semantics as ur3e_batch_step."""
 
-    def __init__(self, model_c, cfg: OracleConfig, n_envs: int):
-        self.L = lib()
+    def __init__(self, model_c, cfg: OracleConfig, n_envs: int, L=None):
+        self.L = lib() if L is None else L
         self.m = model_c
         self.cfg = cfg
         self.n = n_envs

@@ -1,5 +1,5 @@
 """The C-ABI library builds for gfx950, loads, and exports every entry point
-include/ur3e_batch.h declares (no compute calls: no GPU here)."""
+include/*.h declares (no compute calls: no GPU here)."""
 import ctypes
 import os
 import re
@@ -9,8 +9,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _declared():
-    src = open(os.path.join(REPO, "include", "ur3e_batch.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ur3e_\w+)\(", src, re.M)))
+    import glob
+    names = set()
+    for h in sorted(glob.glob(os.path.join(REPO, "include", "*.h"))):
+        src = open(h).read()
+        names |= set(re.findall(r"^\s*(?:int|const char\*)\s+(ur3e_\w+)\(", src, re.M))
+    return sorted(names)
 
 
 def test_library_exports_header_symbols():
@@ -20,7 +24,7 @@ def test_library_exports_header_symbols():
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\bT (ur3e_\w+)", out))
     decl = _declared()
-    assert len(decl) >= 12
+    assert len(decl) >= 15 and "ur3e_vecnorm_step" in decl
     missing = [s for s in decl if s not in exported]
     assert not missing, missing
     L = ctypes.CDLL(lib)

@@ -253,3 +253,41 @@ def test_collect_demos_batched(mode):
     trajs = col.trajectories(torch.from_numpy(obs), torch.from_numpy(acts))
     assert len(trajs) == n and trajs[0].obs.shape[0] == trajs[0].acts.shape[0] + 1
     col.close()
+
+
+@pytest.mark.parametrize("norm_reward", [False, True])
+def test_vecnormalize_gpu_matches_sb3(norm_reward):
+    """On-device VecNormalize (train_rl.py:57) vs the numpy restatement of SB3 2.7.0 on the same raw
+    step outputs: running obs/return statistics, normalised f32 obs, rewards and terminal obs are
+    bit-identical (numpy's axis-0 sequential and 1-D pairwise reduction orders)."""
+    torch = _torch()
+    from oracle.vecnorm_ref import VecNormalizeRef
+    from ur3e_amd.envs.vec_env import UR3eVecEnv
+    from ur3e_amd.envs.vec_normalize import VecNormalize
+    n = 1000  # not a multiple of 8 or 128: exercises every branch of the pairwise sum
+    venv = UR3eVecEnv(num_envs=n, seed=4, max_episode_steps=7)
+    vn = VecNormalize(venv, norm_reward=norm_reward, clip_obs=10.0)
+    ref = VecNormalizeRef(n, 24, norm_reward=norm_reward, clip_obs=10.0)
+    o = vn.reset()
+    np.testing.assert_array_equal(o, ref.reset(vn.get_original_obs()))
+    rng = np.random.default_rng(0)
+    saw_done = False
+    for s in range(20):
+        a = rng.uniform(venv.action_space.low, venv.action_space.high, size=(n, 4))
+        obs, rew, dones, infos = vn.step(a)
+        raw_obs, raw_rew = vn.get_original_obs(), vn.get_original_reward()
+        raw_tobs = vn._last[2].cpu().numpy()
+        r_obs, r_rew, r_tobs = ref.step(raw_obs, raw_rew, dones, raw_tobs)
+        np.testing.assert_array_equal(vn.obs_rms.mean, ref.obs_rms.mean, err_msg=f"obs mean {s}")
+        np.testing.assert_array_equal(vn.obs_rms.var, ref.obs_rms.var, err_msg=f"obs var {s}")
+        assert vn.obs_rms.count == ref.obs_rms.count
+        assert vn.ret_rms.mean[0] == ref.ret_rms.mean and vn.ret_rms.var[0] == ref.ret_rms.var
+        np.testing.assert_array_equal(vn.returns, ref.returns, err_msg=f"returns {s}")
+        assert obs.dtype == np.float32
+        np.testing.assert_array_equal(obs, r_obs, err_msg=f"obs {s}")
+        np.testing.assert_array_equal(rew, r_rew, err_msg=f"reward {s}")
+        for i, t in r_tobs.items():
+            saw_done = True
+            np.testing.assert_array_equal(infos[i]["terminal_observation"], t)
+    assert saw_done
+    vn.close()

@@ -1092,6 +1092,9 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 
+/* error path shared with the other translation units of the library (ur3e_vecnorm.hip) */
+__attribute__((visibility("hidden"))) int ur3e_internal_fail(int code, const char* msg) { return fail(code, msg); }
+
 #define HIPCHK(x)                                                                          \
   do {                                                                                     \
     hipError_t _e = (x);                                                                   \

@@ -64,7 +64,14 @@ class UR3eVecEnv(_SB3VecEnv):
 
     def step_wait(self):
         obs, rew, term, trunc, tobs = self.step_torch(self._actions)
-        obs, rew, term, trunc = _np(obs), _np(rew), _np(term).astype(bool), _np(trunc).astype(bool)
+        obs = _np(obs)
+        rew, dones, infos = self.episode_infos(rew, term, trunc, tobs)
+        return obs, rew, dones, infos
+
+    def episode_infos(self, rew, term, trunc, tobs):
+        """Host-side SB3 bookkeeping of one step: (rewards, dones, infos) with terminal_observation
+        (rows of `tobs` for done envs), TimeLimit.truncated and Monitor's episode {r, l, t}."""
+        rew, term, trunc = _np(rew), _np(term).astype(bool), _np(trunc).astype(bool)
         dones = term | trunc
         self._ep_ret += rew
         self._ep_len += 1
@@ -78,7 +85,7 @@ class UR3eVecEnv(_SB3VecEnv):
                 infos[i]["episode"] = {"r": float(self._ep_ret[i]), "l": int(self._ep_len[i]), "t": now}
                 self._ep_ret[i] = 0
                 self._ep_len[i] = 0
-        return obs, rew, dones, infos
+        return rew, dones, infos
 
     def step(self, actions):
         self.step_async(actions)
