@@ -57,6 +57,10 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
         if s % check_every == 0 or s == steps - 1:
             torch.cuda.synchronize()
             n_done += int(((o_term > 0) | (o_trunc > 0)).sum())
+            qp, qv, wa = gb.get_state()
+            oqp, oqv, owa, onc = ob.get_state()
+            bad = np.flatnonzero((qp.cpu().numpy() != oqp).any(axis=1))
+            assert bad.size == 0, f"qpos step {s}: envs {bad[:10]} ncon gpu {gb.get_info()['ncon'].cpu().numpy()[bad[:10]]} oracle {onc[bad[:10]]}"
             if gym:
                 np.testing.assert_array_equal(g_tobs.cpu().numpy()[o_term | o_trunc > 0],
                                               o_tobs[o_term | o_trunc > 0], err_msg=f"terminal obs step {s}")
@@ -64,8 +68,6 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
                 np.testing.assert_array_equal(g_term.cpu().numpy(), o_term, err_msg=f"terminated step {s}")
                 np.testing.assert_array_equal(g_trunc.cpu().numpy(), o_trunc, err_msg=f"truncated step {s}")
                 np.testing.assert_array_equal(g_obs.cpu().numpy(), o_obs, err_msg=f"obs step {s}")
-            qp, qv, wa = gb.get_state()
-            oqp, oqv, owa, onc = ob.get_state()
             max_dq = max(max_dq, float(np.abs(qp.cpu().numpy() - oqp).max()))
             np.testing.assert_array_equal(qp.cpu().numpy(), oqp, err_msg=f"qpos step {s}")
             np.testing.assert_array_equal(qv.cpu().numpy(), oqv, err_msg=f"qvel step {s}")

@@ -7,7 +7,8 @@ LIB = os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_timing.so")
 if not os.path.exists(LIB):
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
                     "-shared", "-Wno-unused-result", "-DUR3E_STAGE_TIMING", "-o", LIB,
-                    os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip")], check=True)
+                    os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip"),
+                    os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_vecnorm.hip")], check=True)
 os.environ["UR3E_LIB"] = LIB
 import torch
 from ur3e_amd import runtime as rt

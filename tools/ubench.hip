@@ -17,7 +17,7 @@ __device__ __forceinline__ double rl(double v, int lane) {
 // 2: sqrt chain (100), 3: div chain (100)
 // 4: cholesky readlane, 5: cholesky LDS broadcast
 __global__ void kb(int which, double* out, unsigned long long* cyc, int reps) {
-  __shared__ double sh[NV * NV + 64];
+  __shared__ double sh[64 * 16 + NV * NV + 64];
   const int lane = threadIdx.x;
   double v = 1.0 + lane * 1e-3;
   double h[NV];
@@ -53,6 +53,36 @@ __global__ void kb(int which, double* out, unsigned long long* cyc, int reps) {
         f4 = f4 * 1.0000001f; f5 = f5 * 1.0000001f; f6 = f6 * 1.0000001f; f7 = f7 * 1.0000001f;
       }
       v = f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7;
+    } else if (which == 9) {
+      /* dependent LDS pointer chase (ds_read_b32 -> address of the next read), x100 */
+      int* ish = (int*)sh;
+      ish[lane] = (lane + 1) & 63;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      int idx = lane;
+      for (int i = 0; i < 100; i++) { idx = ish[idx]; asm volatile("" : "+v"(idx)); }
+      v += idx;
+    } else if (which == 10) {
+      /* LDS write -> read-back round trip of a double through a neighbour lane, x100 */
+      for (int i = 0; i < 100; i++) {
+        sh[lane] = v;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        v = sh[(lane + 1) & 63] * 1.0000001;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+      }
+    } else if (which == 11) {
+      /* 16 doubles copied parent -> child per "level" (kinematics level loop shape), x20 levels */
+      int pid = lane > 0 ? lane - 1 : 0;
+      for (int l = 1; l <= 20; l++) {
+        if (lane == l) {
+          for (int c = 0; c < 16; c++) sh[lane * 16 + c] = sh[pid * 16 + c] + 1e-9;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+      }
+      v += sh[lane];
     } else if (which == 4) {
 #pragma unroll
       for (int j = 0; j < NV; j++) {
@@ -103,8 +133,9 @@ int main() {
   hipMalloc(&cyc, sizeof(unsigned long long) * 4096);
   const char* names[] = {"fp64 add chain x1000", "rl-sum 20 lanes x50", "sqrt chain x100", "div chain x100",
                          "cholesky20 readlane", "cholesky20 lds-bcast", "fp64 mul 8 indep x125", "fp64 mul dep x1000",
-                         "fp32 mul 8 indep x125"};
-  for (int which = 0; which < 9; which++) {
+                         "fp32 mul 8 indep x125", "lds ptr-chase x100", "lds wr->rd trip x100",
+                         "lds level copy x20"};
+  for (int which = 0; which < 12; which++) {
     for (int grid : {1, 1024}) {
       int reps = 4;
       hipLaunchKernelGGL(kb, dim3(grid), dim3(64), 0, 0, which, out, cyc, 1);

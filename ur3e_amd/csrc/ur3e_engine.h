@@ -579,8 +579,9 @@ KD int k_plane_box(const double pp[3], const double pm[9], const double bp[3], c
   return cnt;
 }
 
-KDN int k_box_box(const double p1[3], const double R1[9], const double s1[3], const double p2[3],
-                  const double R2[9], const double s2[3], double margin, KRaw* out) {
+__device__ static __forceinline__ int k_box_box_inl(const double p1[3], const double R1[9], const double s1[3],
+                                                     const double p2[3], const double R2[9], const double s2[3],
+                                                     double margin, KRaw* out) {
   double a[3][3], b[3][3];
   for (int k = 0; k < 3; k++) {
     a[k][0] = R1[k]; a[k][1] = R1[3 + k]; a[k][2] = R1[6 + k];
@@ -730,6 +731,12 @@ KDN int k_box_box(const double p1[3], const double R1[9], const double s1[3], co
     cnt++;
   }
   return cnt;
+}
+
+/* out-of-line copy for the multi-call-site paths (keeps those kernels' code size down) */
+KDN int k_box_box(const double p1[3], const double R1[9], const double s1[3], const double p2[3],
+                  const double R2[9], const double s2[3], double margin, KRaw* out) {
+  return k_box_box_inl(p1, R1, s1, p2, R2, s2, margin, out);
 }
 
 KDN void k_collision(KModel m, KData* d) {

@@ -141,6 +141,16 @@ __device__ __forceinline__ void wsync() {
 }
 #define SYNC() wsync<NT>()
 #define SYNC64() wsync<64>()
+
+/* any lane of the workgroup has pred set (uniform result) */
+template <int NT>
+__device__ __forceinline__ int w_any(int pred) {
+  if constexpr (NT == 64) {
+    return __ballot(pred) != 0;
+  } else {
+    return __syncthreads_or(pred);
+  }
+}
 #define WD __device__ static __forceinline__
 
 /* diagnostic build only (-DUR3E_STAGE_TIMING): per-stage shader-clock cycles, lane 0 of every env */
@@ -436,8 +446,9 @@ WD void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K
 /* ================================================================== */
 /* collision: per-candidate lanes, prefix offsets, deterministic order */
 /* ================================================================== */
+/* bounding-sphere test of candidate pair p (mj_collideGeoms' rbound early-out) */
 template <class KS>
-WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
+WD bool w_pair_near(KModel m, const KS& s, int p) {
   int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   double margin = m->cpair_margin[p];
   double rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
@@ -446,20 +457,105 @@ WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
     double dy = s.geom_xpos[g1][1] - s.geom_xpos[g2][1];
     double dz = s.geom_xpos[g1][2] - s.geom_xpos[g2][2];
     double lim = rb1 + rb2 + margin;
-    if (dx * dx + dy * dy + dz * dz > lim * lim) return 0;
+    if (dx * dx + dy * dy + dz * dz > lim * lim) return false;
   }
+  return true;
+}
+
+/* narrowphase of candidate pair p (after w_pair_near): raw contacts, returns their count */
+template <class KS, bool INL = false>
+WD int w_narrow_core(KModel m, const KS& s, int p, KRaw* raw) {
+  int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
+  double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
     return k_plane_box(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2], margin,
                        raw);
-  if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX)
-    return k_box_box(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
-                     m->geom_size[g2], margin, raw);
+  if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX) {
+    if constexpr (INL)
+      return k_box_box_inl(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
+                           m->geom_size[g2], margin, raw);
+    else
+      return k_box_box(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
+                       m->geom_size[g2], margin, raw);
+  }
   return 0;
+}
+
+template <class KS>
+WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
+  return w_pair_near(m, s, p) ? w_narrow_core(m, s, p, raw) : 0;
+}
+
+/* contact c of the env from raw contact r of candidate pair p */
+template <class KS>
+WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
+  s.con_pos[c][0] = r.pos[0]; s.con_pos[c][1] = r.pos[1]; s.con_pos[c][2] = r.pos[2];
+  k_make_frame(s.con_frame[c], r.n);
+  s.con_dist[c] = r.dist;
+  s.con_geom1[c] = m->cpair_geom1[p];
+  s.con_geom2[c] = m->cpair_geom2[p];
+  s.con_cpair[c] = p;
+  s.con_mu[c] = 0;
+  s.con_efc[c] = -1;
+}
+
+/* one 64-lane wavefront: bounding-sphere filter over all candidates, survivors compacted in
+   candidate order (ballot + mbcnt), ONE narrowphase per survivor (lane = survivor), contact
+   offsets by a wave prefix scan of the counts, contacts written from the lane's own results.
+   Same contacts in the same order as the count / prefix / write passes of w_collision. */
+template <class KS, int VAR = 0>
+WD void r_collision(KModel m, KS& s) {
+  const int lane = threadIdx.x;
+  const int np = m->ncpair;
+  int nsurv = 0;
+  for (int base = 0; base < np; base += 64) {
+    const int p = base + lane;
+    const bool ok = p < np && w_pair_near(m, s, p);
+    const unsigned long long bm = __ballot(ok);
+    if (ok) s.cand_off[nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] = p;
+    nsurv += __popcll(bm);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  int total = 0;
+  for (int base = 0; base < nsurv; base += 64) {
+    const int slot = base + lane;
+    /* every lane runs the narrowphase (idle lanes on survivor 0, result dropped) and the box-box
+       routine is inlined here: an out-of-line call from this divergent, register-saturated region
+       (256 VGPR + AGPR spill slots + ~760 SGPRs spilled to VGPR lanes) was miscompiled -- state
+       read after the forward pass came back corrupted -- while the inlined form is bit-exact */
+    const bool act = slot < nsurv;
+    const int p = s.cand_off[act ? slot : 0];
+    KRaw raw[8];
+    int cnt = w_narrow_core<KS, true>(m, s, p, raw);
+    cnt = act ? cnt : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    const int off = total + incl - cnt;
+    total += rli(incl, 63);
+    if constexpr (VAR == 1) continue;
+    for (int k = 0; k < cnt && off + k < KS::MAXCON; k++) w_store_contact(m, s, off + k, p, raw[k]);
+  }
+  if (lane == 0) {
+    s.ncon = total < KS::MAXCON ? total : KS::MAXCON;
+    if (KS::BAIL && total > s.cap_con) s.ovf = 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 
 template <int NT, class KS, int VAR = 0>
 WD void w_collision(KModel m, KS& s) {
+  if constexpr (NT == 64) {
+    r_collision<KS, VAR>(m, s);
+    return;
+  }
   const int tid = threadIdx.x;
   const int np = m->ncpair;
   KRaw raw[8];
@@ -482,17 +578,7 @@ WD void w_collision(KModel m, KS& s) {
     int off = s.cand_off[p];
     if (cnt == 0 || off >= KS::MAXCON) continue;
     int n = w_narrow(m, s, p, raw);
-    for (int k = 0; k < n && off + k < KS::MAXCON; k++) {
-      int c = off + k;
-      s.con_pos[c][0] = raw[k].pos[0]; s.con_pos[c][1] = raw[k].pos[1]; s.con_pos[c][2] = raw[k].pos[2];
-      k_make_frame(s.con_frame[c], raw[k].n);
-      s.con_dist[c] = raw[k].dist;
-      s.con_geom1[c] = m->cpair_geom1[p];
-      s.con_geom2[c] = m->cpair_geom2[p];
-      s.con_cpair[c] = p;
-      s.con_mu[c] = 0;
-      s.con_efc[c] = -1;
-    }
+    for (int k = 0; k < n && off + k < KS::MAXCON; k++) w_store_contact(m, s, off + k, p, raw[k]);
   }
   SYNC();
 }
@@ -1387,8 +1473,40 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   else
     w_solve_newton<NT>(m, s);
   WT(15);
-  /* touch sensors (lane = sensor), oracle sensor_touch */
-  if (tid < m->ntouch) {
+  /* touch sensors, oracle sensor_touch: sum over contacts (in contact order) of the normal force
+     of contacts on the sensor's body whose ray hits the site box */
+  if constexpr (NT == 64 && KS::MAXCON <= 16) {
+    /* lane = (sensor, contact): every contact tested at once, then an ordered per-sensor sum with
+       -0.0 (the exact additive identity) for contacts that do not count */
+    const int ts = tid >> 4, ci = tid & 15;
+    double val = -0.0;
+    if (ts < m->ntouch && ci < s.ncon) {
+      const int site = m->touch_site[ts];
+      const int body = m->site_bodyid[site];
+      const int adr = s.con_efc[ci];
+      const int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+      if (adr >= 0 && (body == b1 || body == b2)) {
+        const double fn = s.efc_force[adr];
+        if (fn > 0) {
+          double sp[3], sm[9], ss[3];
+          for (int k = 0; k < 3; k++) { sp[k] = s.site_xpos[site][k]; ss[k] = m->site_size[site][k]; }
+          for (int k = 0; k < 9; k++) sm[k] = s.site_xmat[site][k];
+          double ray[3] = {s.con_frame[ci][0], s.con_frame[ci][1], s.con_frame[ci][2]};
+          if (body == b2) { ray[0] = -ray[0]; ray[1] = -ray[1]; ray[2] = -ray[2]; }
+          double cp[3] = {s.con_pos[ci][0], s.con_pos[ci][1], s.con_pos[ci][2]};
+          if (k_ray_box_hit(sp, sm, ss, cp, ray)) val = fn;
+        }
+      }
+    }
+    const int nt = m->ntouch, nc = s.ncon;
+    double mine = 0;
+    for (int k = 0; k < nt; k++) {
+      double sum = 0;
+      for (int c = 0; c < nc; c++) sum += rl(val, (k << 4) + c);
+      if (tid == k) mine = sum;
+    }
+    if (tid < nt) s.touch[tid] = mine;
+  } else if (tid < m->ntouch) {
     const int site = m->touch_site[tid];
     const int body = m->site_bodyid[site];
     double sp[3], sm[9], ss[3];
@@ -1418,14 +1536,10 @@ template <int NT, class KS>
 WD void w_step_pre(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nq = m->nq, nv = NVOF(KS, m);
-  if (tid == 0) {
-    int bad = 0;
-    for (int k = 0; k < nq; k++) bad |= k_is_bad(s.qpos[k]);
-    for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qvel[k]);
-    s.flag = bad;
-  }
-  SYNC();
-  if (s.flag) {
+  int bad = 0;
+  for (int k = tid; k < nq; k += NT) bad |= k_is_bad(s.qpos[k]);
+  for (int k = tid; k < nv; k += NT) bad |= k_is_bad(s.qvel[k]);
+  if (w_any<NT>(bad)) {
     if (tid < nq) s.qpos[tid] = m->qpos0[tid];
     if (tid < nv) { s.qvel[tid] = 0; s.warm[tid] = 0; }
     if (tid == 0) s.nwarn++;
@@ -1438,13 +1552,9 @@ template <int NT, class KS>
 WD int w_step_badacc(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nq = m->nq, nv = NVOF(KS, m);
-  if (tid == 0) {
-    int bad = 0;
-    for (int k = 0; k < nv; k++) bad |= k_is_bad(s.qacc[k]);
-    s.flag = bad;
-  }
-  SYNC();
-  if (s.flag) {
+  int bad = 0;
+  for (int k = tid; k < nv; k += NT) bad |= k_is_bad(s.qacc[k]);
+  if (w_any<NT>(bad)) {
     if (tid < nq) s.qpos[tid] = m->qpos0[tid];
     if (tid < nv) { s.qvel[tid] = 0; s.warm[tid] = 0; }
     if (tid == 0) s.nwarn++;
