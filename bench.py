@@ -35,34 +35,67 @@ ALGO_BYTES_PER_ENV_STEP = 1898
 FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
-def cpu_baseline(n_envs_sample=4096, steps=200, seed=0):
-    """Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of the same workload."""
+def _state_diff(gb, ob):
+    """max |qpos - ref|, max |qvel - ref| and contact-count mismatches, GPU handle vs oracle batch"""
+    qp, qv, _ = gb.get_state()
+    oqp, oqv, _, onc = ob.get_state()
+    ncon = gb.get_info()["ncon"].cpu().numpy()
+    return dict(max_abs_qpos=float(np.abs(qp.cpu().numpy() - oqp).max()),
+                max_abs_qvel=float(np.abs(qv.cpu().numpy() - oqv).max()),
+                ncon_mismatch_envs=int((ncon != onc).sum()))
+
+
+def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0):
+    """The cpu_baseline leg.  (1) Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of
+    the bench workload: n_envs_sample gym ur3e-v2 envs x `steps` env-steps.  (2) As the checker, replay
+    the same seeded actions through a fresh GPU handle and report the metric's second half,
+    max |qpos - ref| after `steps` env-steps (the oracle is the reference here: MuJoCo is absent)."""
+    import torch
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model("main")
     c = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=seed)
-    oc = po.OracleConfig()
-    for f, _ in po.OracleConfig._fields_:
-        v = getattr(c, f)
-        if f in ("task_gains", "joint_gains"):
-            for k in range(12):
-                getattr(oc, f)[k] = v[k]
-        else:
-            setattr(oc, f, v)
-    ob = po.OracleBatch(mc, oc, n_envs_sample)
+    ob = po.OracleBatch(mc, po.config_from(c), n_envs_sample)
+    gb = rt.Batch(mc, c, n_envs_sample)
     rng = np.random.default_rng(seed)
     lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
     hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
-    acts = [rng.uniform(lo, hi, size=(n_envs_sample, 4)) for _ in range(steps)]
-    ob.step(acts[0])
-    t0 = time.perf_counter()
-    for a in acts:
+    dt = 0.0
+    for _ in range(steps):
+        a = rng.uniform(lo, hi, size=(n_envs_sample, 4))
+        t0 = time.perf_counter()
         ob.step(a)
-    dt = time.perf_counter() - t0
+        dt += time.perf_counter() - t0
+        gb.step(torch.from_numpy(a))
+    torch.cuda.synchronize()
+    parity = dict(workload="gym ur3e-v2, uniform random actions", envs=n_envs_sample, steps=steps,
+                  **_state_diff(gb, ob))
+    gb.close()
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=cores, kind="port",
+    base = dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=cores, kind="port",
                 sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps), "
                        f"oracle/ C restatement, OpenMP {cores} threads, {dt:.1f} s")
+    return base, parity
+
+
+def move_l_mug_parity(n_envs=512, steps=1000, seed=0):
+    """Checker for the north_star's parity clause: the move_l_mug scripted grasp (C3 semantics:
+    pid_task_ctrl along per-env build_traj_l_pick_place rows, one mj_step per row, 'low' mug noise)
+    for `steps` rows on the GPU and on the oracle; max |qpos - ref| and ncon mismatches at the end."""
+    import torch
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    drv = MoveLMug(n_envs, reset_mode="low", seed=seed)
+    gb = drv.batch
+    ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n_envs)
+    for _ in range(steps):
+        row = drv.step()
+        ob.step(row.cpu().numpy())
+    torch.cuda.synchronize()
+    out = dict(workload="move_l_mug scripted pick (main.xml, pid_task_ctrl, 1 substep)", envs=n_envs,
+               steps=steps, **_state_diff(gb, ob))
+    drv.close()
+    return out
 
 
 def main():
@@ -74,7 +107,7 @@ def main():
     ap.add_argument("--envs-per-block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
-    ap.add_argument("--cpu-sample-steps", type=int, default=200)
+    ap.add_argument("--cpu-sample-steps", type=int, default=1000)
     ap.add_argument("--no-gather", action="store_true")
     args = ap.parse_args()
 
@@ -179,10 +212,13 @@ def main():
                         "source": "profiles/flops_r01.json (tools/count_flops.py: counting build of the oracle)"}
             except Exception:
                 fp64 = None
-        cpu = None
+        cpu, parity = None, None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
+                cpu, p_gym = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
+                parity = {"gym_v2": p_gym, "move_l_mug": move_l_mug_parity(steps=args.cpu_sample_steps),
+                          "reference": "oracle/ (CPU restatement; MuJoCo 3.3.3 absent: parity vs MuJoCo unpinned)",
+                          "tolerance": 1e-5}
             except Exception as e:  # the oracle is only the checker; never fail the bench on it
                 cpu = dict(value=None, unit="env-steps/s", cores=None, kind="port", sample=f"failed: {e}")
         line = {
@@ -215,6 +251,7 @@ def main():
                          "note": "path is FP64-latency-bound (SURVEY.md §8d); HBM fraction reported as required"},
             "roofline_fp64": fp64,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line), flush=True)
     batch.close()

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 2
+#define UR3E_ABI_VERSION 3
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -51,6 +51,10 @@ extern "C" {
 #define UR3E_TASK_GYM_V0 4          /* ur3e-v0 (ur3e_env.py): action [N,4], obs [N,13], T = 500 */
 #define UR3E_TASK_IMIT_INDIRECT 5   /* imitation_indirect-v0: action [N,4], obs [N,24], reward -1 */
 #define UR3E_TASK_IMIT_DIRECT 6     /* imitation_direct-v0: action [N,nu] ctrl, obs [N,13], reward -1 */
+/* scripted move_l (controller/move_l.py:15-78): action [N,7] task-space trajectory row; joint deltas
+   pinv(Jp_arm) e_p and pinv(Jr_arm) e_r through two pd_joint_ctrl calls (joint_gains = "pos",
+   rot_joint_gains = "rot" of config_l.yml), summed; 1 physics step per env-step */
+#define UR3E_TASK_MOVE_L 7
 
 /* error codes */
 #define UR3E_OK 0
@@ -68,7 +72,7 @@ typedef struct ur3e_config_t {
                             1 "high" (ur3e-v2), 2 "med", 3 "low" */
   int reset_key;         /* keyframe index used by reset (-1: qpos0) */
   double task_gains[12]; /* kp_pos[3], kd_pos[3], kp_rot[3], kd_rot[3] (config_l_mug.yml) */
-  double joint_gains[12];/* kp[6], kd[6] (config_j.yml) */
+  double joint_gains[12];/* kp[6], kd[6] (config_j.yml; move_l: config_l.yml "pos") */
   unsigned long long seed; /* Philox key for reset noise */
   int env_id_offset;     /* global id of local env 0 (multi-GPU shards) */
   int envs_per_block;    /* kernel layout:
@@ -81,6 +85,7 @@ typedef struct ur3e_config_t {
                             1..64 = one env per lane, that many envs per wavefront (v1) */
   int tier_con_cap;      /* diagnostic (0 = off): the compact tier treats more than this many
                             contacts as overflow, to exercise the fallback path */
+  double rot_joint_gains[12]; /* kp[6], kd[6] of the rotation PD in move_l (config_l.yml "rot") */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;

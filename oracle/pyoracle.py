@@ -37,8 +37,16 @@ class OracleConfig(ctypes.Structure):
         ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
-        ("tier_con_cap", ctypes.c_int),
+        ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
     ]
+
+
+def config_from(cfg) -> OracleConfig:
+    """Copy a runtime.ConfigC (same field layout as ur3e_config_t) into an OracleConfig."""
+    oc = OracleConfig()
+    assert [f for f, _ in type(cfg)._fields_] == [f for f, _ in OracleConfig._fields_], "config layouts differ"
+    ctypes.memmove(ctypes.byref(oc), ctypes.byref(cfg), ctypes.sizeof(OracleConfig))
+    return oc
 
 
 def _p(a):
@@ -160,6 +168,18 @@ def pd_joint_ctrl_raw(q6, v6, delta6, jnt_range12, ctrl_range12, kp6, kd6):
     a = [np.ascontiguousarray(x, dtype=np.float64).reshape(-1) for x in (q6, v6, delta6, jnt_range12, ctrl_range12)]
     out = np.zeros(6)
     L.ur3o_pd_joint_ctrl_raw(*[_p(x) for x in a], _p(g), _p(out))
+    return out
+
+
+def move_l_ctrl_raw(traj7, tcp_xpos, tcp_xmat, jacp_arm, jacr_arm, q6, v6, jnt_range12, ctrl_range12,
+                    pos_kp, pos_kd, rot_kp, rot_kd, grip_scale=255.0):
+    L = lib()
+    gp = np.ascontiguousarray(np.concatenate([pos_kp, pos_kd]), dtype=np.float64)
+    gr = np.ascontiguousarray(np.concatenate([rot_kp, rot_kd]), dtype=np.float64)
+    a = [np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+         for x in (traj7, tcp_xpos, tcp_xmat, jacp_arm, jacr_arm, q6, v6, jnt_range12, ctrl_range12)]
+    out = np.zeros(7)
+    L.ur3o_move_l_ctrl_raw(*[_p(x) for x in a], _p(gp), _p(gr), ctypes.c_double(grip_scale), _p(out))
     return out
 
 

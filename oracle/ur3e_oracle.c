@@ -1709,29 +1709,44 @@ void ur3o_pinv3x6(const double J[18], double P[18]) {
     }
 }
 
-void ur3o_move_l_ctrl(const ur3e_model_t* m, const ur3o_data* d, const double traj[7],
-                      const ur3o_joint_gains* gpos, const ur3o_joint_gains* grot, double* ctrl) {
-  /* controller/move_l.py:15-78 */
-  int nv = m->nv, s = m->id_site_tcp;
-  double jp[3 * UR3E_MAXNV], jrr[3 * UR3E_MAXNV], Jp[18], Jr[18], Pp[18], Pr[18];
-  ur3o_jac_site(m, d, s, jp, jrr);
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 6; c++) { Jp[6 * r + c] = jp[r * nv + c]; Jr[6 * r + c] = jrr[r * nv + c]; }
+void ur3o_move_l_ctrl_raw(const double traj[7], const double tcp_xpos[3], const double tcp_xmat[9],
+                          const double Jp[18], const double Jr[18], const double q[6], const double v[6],
+                          const double jr[12], const double cr[12], const ur3o_joint_gains* gpos,
+                          const ur3o_joint_gains* grot, double grip_scale, double ctrl[7]) {
+  /* controller/move_l.py:15-78: get_pos_joint_delta (:35-55) = pinv(jacp_arm) e_p,
+     get_rot_joint_delta (:58-78) = pinv(jacr_arm) e_r, each through pd_joint_ctrl
+     (controller_func.py:128-167) with its own gains, summed (:24-31); grip_ctrl on traj[6] */
+  double Pp[18], Pr[18];
   ur3o_pinv3x6(Jp, Pp);
   ur3o_pinv3x6(Jr, Pr);
-  double ep[3] = {traj[0] - d->site_xpos[s][0], traj[1] - d->site_xpos[s][1], traj[2] - d->site_xpos[s][2]};
+  double ep[3] = {traj[0] - tcp_xpos[0], traj[1] - tcp_xpos[1], traj[2] - tcp_xpos[2]};
   double er[3];
-  ur3o_rot_err(d->site_xmat[s], traj + 3, er);
-  double dp[6], dr[6], jr[12], cr[12], up[6], ur[6];
+  ur3o_rot_err(tcp_xmat, traj + 3, er);
+  double dp[6], dr[6], up[6], ur[6];
   for (int k = 0; k < 6; k++) {
     dp[k] = Pp[3 * k] * ep[0] + Pp[3 * k + 1] * ep[1] + Pp[3 * k + 2] * ep[2];
     dr[k] = Pr[3 * k] * er[0] + Pr[3 * k + 1] * er[1] + Pr[3 * k + 2] * er[2];
   }
-  arm_ranges(m, jr, cr);
-  ur3o_pd_joint_ctrl_raw(d->qpos, d->qvel, dp, jr, cr, gpos, up);
-  ur3o_pd_joint_ctrl_raw(d->qpos, d->qvel, dr, jr, cr, grot, ur);
+  ur3o_pd_joint_ctrl_raw(q, v, dp, jr, cr, gpos, up);
+  ur3o_pd_joint_ctrl_raw(q, v, dr, jr, cr, grot, ur);
   for (int k = 0; k < 6; k++) ctrl[k] = up[k] + ur[k];
-  if (m->nu > 6) ctrl[6] = traj[6] * m->act_ctrlrange[m->nu - 1][1];
+  ctrl[6] = traj[6] * grip_scale;
+}
+
+void ur3o_move_l_ctrl(const ur3e_model_t* m, const ur3o_data* d, const double traj[7],
+                      const ur3o_joint_gains* gpos, const ur3o_joint_gains* grot, double* ctrl) {
+  /* mj_jacSite on the stale kinematics MjData holds after mj_step (move_l.py:47,70), fresh q / qdot */
+  int nv = m->nv, s = m->id_site_tcp;
+  double jp[3 * UR3E_MAXNV], jrr[3 * UR3E_MAXNV], Jp[18], Jr[18];
+  ur3o_jac_site(m, d, s, jp, jrr);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 6; c++) { Jp[6 * r + c] = jp[r * nv + c]; Jr[6 * r + c] = jrr[r * nv + c]; }
+  double jr[12], cr[12], out[7];
+  arm_ranges(m, jr, cr);
+  ur3o_move_l_ctrl_raw(traj, d->site_xpos[s], d->site_xmat[s], Jp, Jr, d->qpos, d->qvel, jr, cr, gpos, grot,
+                       m->act_ctrlrange[m->nu - 1][1], out);
+  for (int k = 0; k < 6; k++) ctrl[k] = out[k];
+  if (m->nu > 6) ctrl[6] = out[6];
 }
 
 /* ===================================================================== */

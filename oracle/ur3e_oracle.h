@@ -175,6 +175,10 @@ void ur3o_move_j_ctrl(const ur3e_model_t* m, const ur3o_data* d, const double tr
 void ur3o_pinv3x6(const double J[18], double P[18]);
 void ur3o_move_l_ctrl(const ur3e_model_t* m, const ur3o_data* d, const double traj7[7],
                       const ur3o_joint_gains* gpos, const ur3o_joint_gains* grot, double* ctrl);
+void ur3o_move_l_ctrl_raw(const double traj[7], const double tcp_xpos[3], const double tcp_xmat[9],
+                          const double Jp[18], const double Jr[18], const double q[6], const double v[6],
+                          const double jr[12], const double cr[12], const ur3o_joint_gains* gpos,
+                          const ur3o_joint_gains* grot, double grip_scale, double ctrl[7]);
 
 /* ---- UR3eEnv2 epilogue ---- */
 void ur3o_obs_v2(const ur3e_model_t* m, const ur3o_data* d, double obs[24]);

@@ -13,6 +13,8 @@
  *   task 2 (move_j):       pd_joint_ctrl on a [7] joint-target row + 1 mj_step
  *                          (controller/move_j.py:76-86).
  *   task 3 (ctrl):         raw ctrl row [nu] + frame_skip mj_step.
+ *   task 7 (move_l):       move_l.ctrl on a [7] trajectory row (pinv joint deltas through two
+ *                          pd_joint_ctrl calls) + 1 mj_step (controller/move_l.py:15-31,130-140).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -33,6 +35,7 @@ typedef struct {
   int env_id_offset;
   int envs_per_block;
   int tier_con_cap;
+  double rot_joint_gains[12];
 } ur3o_config;
 
 /* the model has the sites the 24-d observation reads (main.xml) */
@@ -42,7 +45,7 @@ static int has_obs_sites(const ur3e_model_t* m) {
 
 /* tasks (include/ur3e_batch.h): 0 gym v2, 1 traj_l, 2 move_j, 3 ctrl, 4 gym v0, 5 imitation
    indirect, 6 imitation direct */
-static int is_gym(int task) { return task == 0 || task >= 4; }
+static int is_gym(int task) { return task == 0 || (task >= 4 && task <= 6); }
 int ur3o_obs_dim(int task) { return (task == 4 || task == 6) ? 13 : 24; }
 static void task_obs(const ur3e_model_t* m, const ur3o_data* d, int task, double* obs) {
   if (task == 4) ur3o_obs_v0(m, d, obs);
@@ -110,6 +113,11 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
   ur3o_task_gains tg;
   ur3o_joint_gains jg;
   gains_from_cfg(c, &tg, &jg);
+  ur3o_joint_gains rg;
+  for (int k = 0; k < 6; k++) {
+    rg.kp[k] = c->rot_joint_gains[k];
+    rg.kd[k] = c->rot_joint_gains[6 + k];
+  }
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < n; i++) {
     ur3o_env* e = &envs[i];
@@ -134,7 +142,7 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
       }
       continue;
     }
-    if (c->task >= 4) {
+    if (c->task >= 4 && c->task <= 6) {
       /* ur3e-v0 (ur3e_env.py:139-170), imitation indirect (imitation_env_indirect.py:73-106) and
          direct (imitation_env_direct.py:74-108): truncation tests t before the increment */
       if (c->task == 6) {
@@ -166,6 +174,8 @@ void ur3o_batch_step(const ur3e_model_t* m, const ur3o_config* c, int n, ur3o_en
     }
     if (c->task == 1) {
       ur3o_pid_task_ctrl(m, d, a, &tg, ctrl);
+    } else if (c->task == 7) {
+      ur3o_move_l_ctrl(m, d, a, &jg, &rg, ctrl);
     } else if (c->task == 2) {
       ur3o_move_j_ctrl(m, d, a, &jg, ctrl);
     } else {

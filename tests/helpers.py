@@ -5,15 +5,7 @@ import numpy as np
 
 
 def oracle_config(po, c):
-    oc = po.OracleConfig()
-    for f, _ in po.OracleConfig._fields_:
-        v = getattr(c, f)
-        if f in ("task_gains", "joint_gains"):
-            for k in range(12):
-                getattr(oc, f)[k] = v[k]
-        else:
-            setattr(oc, f, v)
-    return oc
+    return po.config_from(c)
 
 
 class OracleStepper:

@@ -28,7 +28,7 @@ def test_library_exports_header_symbols():
     missing = [s for s in decl if s not in exported]
     assert not missing, missing
     L = ctypes.CDLL(lib)
-    assert L.ur3e_abi_version() == 2
+    assert L.ur3e_abi_version() == 3
     for s in decl:
         getattr(L, s)
 
@@ -43,13 +43,18 @@ def test_code_object_is_gfx950():
 def test_model_struct_layout_matches_header():
     """ctypes mirror == C struct: the oracle (plain C) reports its sizeof view through a probe."""
     from ur3e_amd.model.compiler import UR3eModelC
+    from ur3e_amd.runtime import ConfigC
+    from oracle.pyoracle import OracleConfig
     src = (
-        '#include <stdio.h>\n#include "include/ur3e_model.h"\n'
-        'int main(){printf("%zu\\n", sizeof(ur3e_model_t));return 0;}\n')
+        '#include <stdio.h>\n#include <stddef.h>\n#include "include/ur3e_batch.h"\n'
+        'int main(){printf("%zu %zu %zu\\n", sizeof(ur3e_model_t), sizeof(ur3e_config_t), '
+        'offsetof(ur3e_config_t, rot_joint_gains));return 0;}\n')
     exe = os.path.join(REPO, "oracle", "_build", "sizeof_probe")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     cfile = exe + ".c"
     open(cfile, "w").write(src)
     subprocess.run(["gcc", "-I", REPO, "-o", exe, cfile], check=True)
-    n = int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+    n, nc, off = map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split())
     assert n == ctypes.sizeof(UR3eModelC)
+    assert nc == ctypes.sizeof(ConfigC) == ctypes.sizeof(OracleConfig)
+    assert off == ConfigC.rot_joint_gains.offset

@@ -21,6 +21,21 @@ def test_traj_j_golden(golden):
         np.testing.assert_array_equal(tr[::120], golden["trajj_rows"][i])
 
 
+def test_traj_l_golden(golden):
+    hold = int(golden["trajl_hold"])
+    for i in range(len(golden["trajl_start"])):
+        tr = bt.build_traj_l(golden["trajl_start"][i], hold)
+        assert tr.shape == (500 * hold, 7)
+        np.testing.assert_array_equal(tr[::hold], golden["trajl_rows"][i])
+
+
+def test_move_l_gains_match_config_l(golden):
+    """runtime.GAINS_L_POS / GAINS_L_ROT are controller/config/config_l.yml's "pos" / "rot" PD gains."""
+    from ur3e_amd import runtime as rt
+    np.testing.assert_array_equal([rt.GAINS_L_POS["kp"], rt.GAINS_L_POS["kd"]], golden["cfgl_pos"])
+    np.testing.assert_array_equal([rt.GAINS_L_ROT["kp"], rt.GAINS_L_ROT["kd"]], golden["cfgl_rot"])
+
+
 def test_pick_place_torch_rows(golden):
     s = torch.from_numpy(golden["pp_start"])
     picks = torch.from_numpy(golden["pp_dest"][:, 0])

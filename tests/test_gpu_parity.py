@@ -18,15 +18,7 @@ def _torch():
 
 
 def _oracle_cfg(po, c):
-    oc = po.OracleConfig()
-    for f, _ in po.OracleConfig._fields_:
-        v = getattr(c, f)
-        if f in ("task_gains", "joint_gains"):
-            for k in range(12):
-                getattr(oc, f)[k] = v[k]
-        else:
-            setattr(oc, f, v)
-    return oc
+    return po.config_from(c)
 
 
 def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1, tier_con_cap=0,
@@ -42,7 +34,7 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
     gb = rt.Batch(mc, cfg, n)
     ob = po.OracleBatch(mc, _oracle_cfg(po, cfg), n)
     gobs = gb.obs.cpu().numpy()
-    gym = task == rt.TASK_GYM_V2 or task >= rt.TASK_GYM_V0
+    gym = task in (rt.TASK_GYM_V2, rt.TASK_GYM_V0, rt.TASK_IMIT_INDIRECT, rt.TASK_IMIT_DIRECT)
     assert gb.obs_dim == ob.od
     if gym:
         np.testing.assert_array_equal(gobs, ob.obs)
@@ -132,6 +124,45 @@ def test_move_j_2f85():
         a[:, 6] = rng.uniform(0, 1, size=n)
         return a
     _run_pair("ur3e_2f85", 2, 64, 100, act)
+
+
+def _traj_follower(rows, n, noise, seed=3):
+    """action_fn replaying trajectory rows (one row per env-step, row index = step), with a fixed
+    per-env offset on the position columns so the envs differ"""
+    off = np.random.default_rng(seed).normal(size=(n, 3)) * noise
+    state = {"t": 0}
+
+    def act(rng, n_, md):
+        r = rows[min(state["t"], len(rows) - 1)]
+        state["t"] += 1
+        a = np.tile(r, (n_, 1))
+        a[:, :3] += off
+        return a
+    return act
+
+
+def test_move_l_2f85_traj_l():
+    """move_l.main (controller/move_l.py:88-140) on ur3e_2f85: build_traj_l rows (seed 49 cubic path)
+    through the move_l controller (pinv joint deltas + two pd_joint_ctrl calls), 1 physics step per
+    row, bit-exact vs the oracle.  The trajectory starts at the tcp pose of the reset state."""
+    from ur3e_amd import runtime as rt
+    from ur3e_amd.controller import build_traj as bt
+    _torch()
+    md, mc = rt.load_model("ur3e_2f85")
+    probe = rt.Batch(mc, rt.make_config(task=rt.TASK_MOVE_L, model=md, reset_noise=None), 1)
+    c = probe.get_carry().cpu().numpy()[0]
+    probe.close()
+    start = np.concatenate([c[0:3], [-1.209, -1.209, 1.209], [0.0]])
+    rows = bt.build_traj_l(start, 1)  # one row per env-step (hold 1 keeps the 500-row path short)
+    _run_pair("ur3e_2f85", rt.TASK_MOVE_L, 32, 300, _traj_follower(rows, 32, 0.01), check_every=5)
+
+
+def test_move_j_raw_traj_j():
+    """Config 1 (BASELINE.json configs[0]): ur3e_raw (arm only, dt 1e-4, qpos0 = 0), move_j PD with
+    config_j.yml gains along build_traj_j(0, hold) rows; grip column dropped (nu = 6)."""
+    from ur3e_amd.controller import build_traj as bt
+    rows = bt.build_traj_j(np.zeros(7), 2)
+    _run_pair("ur3e_raw", 2, 16, 400, _traj_follower(rows, 16, 0.0), check_every=10)
 
 
 def test_ctrl_raw():

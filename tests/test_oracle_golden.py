@@ -37,6 +37,19 @@ def test_pinv(golden):
         np.testing.assert_allclose(po.pinv3x6(J), P, rtol=1e-9, atol=1e-12)
 
 
+def test_move_l_ctrl(golden):
+    """move_l.ctrl (controller/move_l.py:15-78) on synthetic MjData: the oracle's normal-equation
+    pinv (the formula the HIP kernel evaluates bit-identically) vs the reference's np.linalg.pinv (SVD)."""
+    jr = golden["movej_jnt_range"].reshape(12)
+    cr = golden["movej_ctrl_range"][:6].reshape(12)
+    pos, rot = golden["cfgl_pos"], golden["cfgl_rot"]
+    for i in range(len(golden["movel_u"])):
+        u = po.move_l_ctrl_raw(golden["movel_traj"][i], golden["movel_xpos"][i], golden["movel_xmat"][i],
+                               golden["movel_jacp"][i], golden["movel_jacr"][i], golden["movel_q"][i],
+                               golden["movel_v"][i], jr, cr, pos[0], pos[1], rot[0], rot[1])
+        np.testing.assert_allclose(u, golden["movel_u"][i], rtol=1e-9, atol=1e-9)
+
+
 def test_reward(golden):
     for o, a, r in zip(golden["rew_obs"], golden["rew_act"], golden["rew"]):
         assert po.reward_v2(o, a) == pytest.approx(r, rel=1e-13, abs=1e-13)

@@ -27,14 +27,7 @@ def main(n=64, steps=100, out_path=None):
     L.ur3f_get_flops.restype = ctypes.c_ulonglong
     md, mc = rt.load_model("main")
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=0)
-    oc = po.OracleConfig()
-    for f, _ in po.OracleConfig._fields_:
-        v = getattr(cfg, f)
-        if f in ("task_gains", "joint_gains"):
-            for k in range(12):
-                getattr(oc, f)[k] = v[k]
-        else:
-            setattr(oc, f, v)
+    oc = po.config_from(cfg)
     ob = po.OracleBatch(mc, oc, n, L=L)
     # cross-check: the counting build computes the same numbers as the plain oracle
     ref = po.OracleBatch(mc, oc, n)

@@ -411,6 +411,20 @@ def main():
     out["aug_start"], out["aug_dest"], out["aug_seed"] = np.array(aug_start), np.array(aug_dest), np.array(aug_seed)
     out["aug_idx"], out["aug_rows"] = aug_idx, np.array(aug_rows)
 
+    # ---- J. build_traj_l (build_traj.py:310-384: np.random.seed(49) cubic task-space path, hold from
+    #      config_l.yml) and the config_l.yml gains move_l.main loads (move_l.py:93-95)
+    tl = []
+    lstarts = [np.array([0.29799994, 0.13349916, 0.1682003, -1.20920499, -1.20920054, 1.20920054, 0.0]),
+               np.concatenate([rng.uniform([0.2, -0.1, 0.2], [0.4, 0.2, 0.5]), rng.normal(size=3), [0.0]])]
+    for s in lstarts:
+        tr = bt.build_traj_l(s.copy(), YML_L["hold"])
+        assert tr.shape == (500 * YML_L["hold"], 7)
+        assert np.all(tr.reshape(-1, YML_L["hold"], 7) == tr[::YML_L["hold"]][:, None, :])
+        tl.append(tr[::YML_L["hold"]])
+    out["trajl_start"], out["trajl_rows"], out["trajl_hold"] = np.array(lstarts), np.array(tl), np.array(YML_L["hold"])
+    out["cfgl_pos"] = np.array([YML_L["pos"]["kp"], YML_L["pos"]["kd"]], dtype=np.float64)
+    out["cfgl_rot"] = np.array([YML_L["rot"]["kp"], YML_L["rot"]["kd"]], dtype=np.float64)
+
     os.makedirs(OUT, exist_ok=True)
     np.savez_compressed(os.path.join(OUT, "reference_golden.npz"), **out)
     meta = {"generator": "tools/make_golden.py", "reference": "derekc22/UR3e @ /root/reference",

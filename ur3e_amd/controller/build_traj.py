@@ -8,6 +8,10 @@
   reference, `destinations` are not mutated in place.
 * build_traj_j               (build_traj.py:387-470): np.random.seed(42) control
   points + cubic interp1d, 500 samples, held `hold` times, grip 0.
+* build_traj_l               (build_traj.py:310-384): np.random.seed(49) task-space
+  control points + cubic interp1d for x, y, z (the rotation draws are made and
+  then overwritten with the fixed rotvec (-1.209, -1.209, 1.209)), grip 1, 500
+  samples held `hold` times -- the move_l.main trajectory (controller/move_l.py:103).
 * build_traj_l_pick_place_imitation_augmented (build_traj.py:61-125): seven
   15-point segments held 100 rows each (pick at start height / down / grab /
   up +0.15 / place / descend +0.025 / drop), uniform noise u/40 or u/20 on all
@@ -79,6 +83,24 @@ def build_traj_j(start, hold):
                                rs.uniform(bounds[j][0], bounds[j][1], ncp)])
         cols.append(interp1d(t_control, ctrl, kind="cubic")(t))
     g = np.tile([0, 0, 0], num_points // 3 + 1)[:num_points]
+    return np.repeat(np.vstack(cols + [g]).T, repeats=hold, axis=0)
+
+
+def build_traj_l(start, hold):
+    from scipy.interpolate import interp1d
+    num_points = 500
+    t = np.linspace(0, 1, num_points)
+    rs = np.random.RandomState(49)  # same MT19937 stream as np.random.seed(49)
+    bounds = [[0.2, 0.5], [-0.3, 0.3], [0.4, 0.8], [-0.1, 0.1], [-0.1, 0.1], [-np.pi / 4, np.pi / 4]]
+    ncp = 10
+    t_control = np.linspace(0, 1, ncp + 1)
+    start = np.asarray(start, dtype=np.float64)
+    # all six control-point draws happen (in x, y, z, rx, ry, rz order) before the rotation columns are
+    # replaced by constants, so the MT19937 stream advances exactly as in the reference
+    ctrl = [np.concatenate([start[j:j + 1], rs.uniform(bounds[j][0], bounds[j][1], ncp)]) for j in range(6)]
+    cols = [interp1d(t_control, ctrl[j], kind="cubic")(t) for j in range(3)]
+    cols += [np.full(num_points, -1.209), np.full(num_points, -1.209), np.full(num_points, 1.209)]
+    g = np.tile([1, 1, 1], num_points // 3 + 1)[:num_points]
     return np.repeat(np.vstack(cols + [g]).T, repeats=hold, axis=0)
 
 

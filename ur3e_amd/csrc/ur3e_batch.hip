@@ -105,6 +105,7 @@ KD void k_rot_err(const double xmat[9], const double target[3], double err[3]) {
 struct KGains {
   double task[12];
   double joint[12];
+  double rot[12]; /* move_l rotation PD (config_l.yml "rot"); joint[] holds its "pos" gains */
 };
 
 /* pid_task_ctrl (controller_func.py:68-117): carry = [tcp_xpos 3, tcp_xmat 9, J 36, bias 6] */
@@ -132,6 +133,78 @@ KD void k_pid_task_ctrl(const double traj[7], const double* carry, const double 
     ctrl[c] = s + bias[c];
   }
   ctrl[6] = traj[6] * grip_scale;
+}
+
+/* pinv of a full-row-rank 3x6 arm Jacobian block, J' (J J')^-1 with the 3x3 inverse by cofactors;
+   np.linalg.pinv (SVD) in move_l.py:49,72 -- same operation order as oracle ur3o_pinv3x6 */
+KD void k_pinv3x6(const double* J, double P[18]) {
+  double A[9];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      double s = 0;
+      for (int k = 0; k < 6; k++) s += J[6 * r + k] * J[6 * c + k];
+      A[3 * r + c] = s;
+    }
+  double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+  double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+  double inv[9];
+  inv[0] = c00 / det;
+  inv[3] = c01 / det;
+  inv[6] = c02 / det;
+  inv[1] = (A[2] * A[7] - A[1] * A[8]) / det;
+  inv[4] = (A[0] * A[8] - A[2] * A[6]) / det;
+  inv[7] = (A[1] * A[6] - A[0] * A[7]) / det;
+  inv[2] = (A[1] * A[5] - A[2] * A[4]) / det;
+  inv[5] = (A[2] * A[3] - A[0] * A[5]) / det;
+  inv[8] = (A[0] * A[4] - A[1] * A[3]) / det;
+  for (int k = 0; k < 6; k++)
+    for (int c = 0; c < 3; c++) {
+      double s = 0;
+      for (int r = 0; r < 3; r++) s += J[6 * r + k] * inv[3 * r + c];
+      P[3 * k + c] = s;
+    }
+}
+
+/* pd_joint_ctrl (controller_func.py:128-167): target = clip(q + delta, jnt_range), u = kp e - kd qdot,
+   clipped to the actuator ctrlrange */
+KD void k_pd_joint(KModel m, const double* q, const double* v, const double delta[6], const double* g,
+                   double u[6]) {
+  for (int k = 0; k < 6; k++) {
+    double t = q[k] + delta[k];
+    if (t < m->jnt_range[k][0]) t = m->jnt_range[k][0];
+    if (t > m->jnt_range[k][1]) t = m->jnt_range[k][1];
+    double e = t - q[k];
+    double uk = g[k] * e + g[6 + k] * (-v[k]);
+    if (uk < m->act_ctrlrange[k][0]) uk = m->act_ctrlrange[k][0];
+    if (uk > m->act_ctrlrange[k][1]) uk = m->act_ctrlrange[k][1];
+    u[k] = uk;
+  }
+}
+
+/* move_l.ctrl (controller/move_l.py:15-78): delta_p = pinv(Jp_arm) e_p (get_pos_joint_delta),
+   delta_r = pinv(Jr_arm) e_r (get_rot_joint_delta), each through pd_joint_ctrl with its own gains,
+   summed; grip_ctrl on traj[6].  Jacobian, tcp pose: the stale-kinematics carry, as mj_jacSite reads
+   them after mj_step; q, qdot fresh */
+KD void k_move_l_ctrl(KModel m, const double traj[7], const double* carry, const double* q, const double* v,
+                      const KGains& g, double* ctrl) {
+  const double* tcp_xpos = carry;
+  const double* tcp_xmat = carry + 3;
+  const double* J = carry + 12; /* [jacp; jacr] 6x6 row-major */
+  double Pp[18], Pr[18];
+  k_pinv3x6(J, Pp);
+  k_pinv3x6(J + 18, Pr);
+  double ep[3] = {traj[0] - tcp_xpos[0], traj[1] - tcp_xpos[1], traj[2] - tcp_xpos[2]};
+  double er[3];
+  k_rot_err(tcp_xmat, traj + 3, er);
+  double dp[6], dr[6], up[6], ur[6];
+  for (int k = 0; k < 6; k++) {
+    dp[k] = Pp[3 * k] * ep[0] + Pp[3 * k + 1] * ep[1] + Pp[3 * k + 2] * ep[2];
+    dr[k] = Pr[3 * k] * er[0] + Pr[3 * k + 1] * er[1] + Pr[3 * k + 2] * er[2];
+  }
+  k_pd_joint(m, q, v, dp, g.joint, up);
+  k_pd_joint(m, q, v, dr, g.rot, ur);
+  for (int k = 0; k < 6; k++) ctrl[k] = up[k] + ur[k];
+  if (m->nu > 6) ctrl[6] = traj[6] * m->act_ctrlrange[m->nu - 1][1];
 }
 
 /* move_j = pd_joint_ctrl on delta = target - q (move_j.py:14-38, controller_func.py:128-167) */
@@ -406,7 +479,10 @@ __global__ __launch_bounds__(64) void k_env_step(const ur3e_model_t* __restrict_
   for (int k = 0; k < adim && k < 8; k++) a[k] = actions[(size_t)e * adim + k];
   double ctrl[K_NU];
   double carry[NCARRY];
-  if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
+  if (c.task == UR3E_TASK_MOVE_L) {
+    for (int k = 0; k < NCARRY; k++) carry[k] = s.carry[SC(s, k, e)];
+    k_move_l_ctrl(m, a, carry, d.qpos, d.qvel, c.gains, ctrl);
+  } else if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L) {
     for (int k = 0; k < NCARRY; k++) carry[k] = s.carry[SC(s, k, e)];
     double traj[7];
     if (c.task == UR3E_TASK_GYM_V2) {
@@ -702,7 +778,9 @@ KD int k_termination_v0(KModel m, const double obs[13], int selfcol) {
   return 0;
 }
 
-KD int k_is_gym(int task) { return task == UR3E_TASK_GYM_V2 || task >= UR3E_TASK_GYM_V0; }
+KD int k_is_gym(int task) {
+  return task == UR3E_TASK_GYM_V2 || (task >= UR3E_TASK_GYM_V0 && task <= UR3E_TASK_IMIT_DIRECT);
+}
 __host__ __device__ static inline int k_obs_dim(int task) { return (task == UR3E_TASK_GYM_V0 || task == UR3E_TASK_IMIT_DIRECT) ? 13 : 24; }
 
 /* the task's observation into obs (lane 0) */
@@ -836,6 +914,8 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       k_pid_task_ctrl(traj, o.carry, s.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
       for (int k = 0; k < 6; k++) ctrl[k] = out[k];
       if (m->nu > 6) ctrl[6] = out[6];
+    } else if (c.task == UR3E_TASK_MOVE_L) {
+      k_move_l_ctrl(m, o.a, o.carry, s.qpos, s.qvel, c.gains, ctrl);
     } else if (c.task == UR3E_TASK_MOVE_J) {
       for (int k = 0; k < 6; k++) {
         double q = s.qpos[k];
@@ -1162,17 +1242,19 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   if (!model || !cfg || !out || n_envs <= 0) return fail(UR3E_EINVAL, "null argument or n_envs <= 0");
   int rc = check_model(model);
   if (rc) return rc;
-  if (cfg->task < 0 || cfg->task > 6) return fail(UR3E_EINVAL, "unknown task");
-  if (cfg->task >= UR3E_TASK_GYM_V0 && cfg->envs_per_block > 0)
+  if (cfg->task < 0 || cfg->task > UR3E_TASK_MOVE_L) return fail(UR3E_EINVAL, "unknown task");
+  const int gym_other = cfg->task >= UR3E_TASK_GYM_V0 && cfg->task <= UR3E_TASK_IMIT_DIRECT;
+  if (gym_other && cfg->envs_per_block > 0)
     return fail(UR3E_EINVAL, "ur3e-v0 / imitation tasks need a workgroup-per-env layout (envs_per_block <= 0)");
-  if (cfg->task >= UR3E_TASK_GYM_V0 && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
+  if (gym_other && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
                                         model->id_body_ghost < 0 || model->id_body_fish < 0 ||
                                         model->id_site_rpad < 0))
     return fail(UR3E_EMODEL, "ur3e-v0 / imitation tasks need assets/main.xml");
   if (cfg->task == UR3E_TASK_GYM_V2 && (model->id_site_tcp < 0 || model->id_site_handle < 0 ||
                                         model->id_body_ghost < 0 || model->id_body_fish < 0))
     return fail(UR3E_EMODEL, "gym ur3e-v2 task needs tcp/handle_site/ghost/fish (assets/main.xml)");
-  if ((cfg->task == UR3E_TASK_GYM_V2 || cfg->task == UR3E_TASK_TRAJ_L) && model->id_site_tcp < 0)
+  if ((cfg->task == UR3E_TASK_GYM_V2 || cfg->task == UR3E_TASK_TRAJ_L || cfg->task == UR3E_TASK_MOVE_L) &&
+      model->id_site_tcp < 0)
     return fail(UR3E_EMODEL, "task-space control needs the tcp site");
   if (cfg->reset_key >= model->nkey) return fail(UR3E_EINVAL, "reset_key out of range");
   if (cfg->envs_per_block > 64) return fail(UR3E_EINVAL, "envs_per_block > 64");
@@ -1206,7 +1288,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->main_tree = model->nv == UR3E_MAIN_NV;
   for (int i = 0; i < model->nv && b->main_tree; i++)
     if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) b->main_tree = 0;
-  for (int k = 0; k < 12; k++) { c.gains.task[k] = cfg->task_gains[k]; c.gains.joint[k] = cfg->joint_gains[k]; }
+  for (int k = 0; k < 12; k++) {
+    c.gains.task[k] = cfg->task_gains[k];
+    c.gains.joint[k] = cfg->joint_gains[k];
+    c.gains.rot[k] = cfg->rot_joint_gains[k];
+  }
   KState& s = b->st;
   s.n = n_envs;
   if (wave_nt) {

@@ -24,6 +24,7 @@ ASSETS = os.path.join(_HERE, "assets")
 
 TASK_GYM_V2, TASK_TRAJ_L, TASK_MOVE_J, TASK_CTRL = 0, 1, 2, 3
 TASK_GYM_V0, TASK_IMIT_INDIRECT, TASK_IMIT_DIRECT = 4, 5, 6
+TASK_MOVE_L = 7
 
 # controller/config/config_l_mug.yml (used by UR3eEnv2, ur3e_env2.py:66-68)
 GAINS_L_MUG = dict(kp_pos=[220.0, 220.0, 120.0], kd_pos=[20.0, 20.0, 40.0],
@@ -33,6 +34,9 @@ GAINS_V0 = dict(kp_pos=[320.0, 320.0, 320.0], kd_pos=[20.0, 20.0, 25.0],
                 kp_rot=[325.0, 325.0, 325.0], kd_rot=[2.0, 2.0, 2.0])
 # controller/config/config_j.yml (move_j)
 GAINS_J = dict(kp=[20.0, 380.0, 300.0, 20.0, 30.0, 10.0], kd=[5.0] * 6)
+# controller/config/config_l.yml (move_l: "pos" and "rot" joint-space PD gains)
+GAINS_L_POS = dict(kp=[20.0, 60.0, 20.0, 20.0, 20.0, 10.0], kd=[5.0, 15.0, 5.0, 5.0, 5.0, 20.0])
+GAINS_L_ROT = dict(kp=[5.02, 5.01, 5.80, 5.80, 5.09, 5.80], kd=[5.0, 50.0, 10.0, 5.0, 5.0, 5.0])
 
 _lib = None
 
@@ -43,7 +47,7 @@ class ConfigC(ctypes.Structure):
         ("auto_reset", ctypes.c_int), ("reset_noise", ctypes.c_int), ("reset_key", ctypes.c_int),
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
-        ("tier_con_cap", ctypes.c_int),
+        ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
     ]
 
 
@@ -89,7 +93,7 @@ def load_model(name: str = "main"):
 
 def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
                 reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
-                task_gains=None, joint_gains=None, tier_con_cap=0) -> ConfigC:
+                task_gains=None, joint_gains=None, tier_con_cap=0, rot_joint_gains=None) -> ConfigC:
     c = ConfigC()
     c.task = task
     c.frame_skip = frame_skip
@@ -103,11 +107,14 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.reset_key = reset_key
     tg = task_gains or GAINS_L_MUG
     g = list(tg["kp_pos"]) + list(tg["kd_pos"]) + list(tg["kp_rot"]) + list(tg["kd_rot"])
-    jg = joint_gains or GAINS_J
+    jg = joint_gains or (GAINS_L_POS if task == TASK_MOVE_L else GAINS_J)
     j = list(jg["kp"]) + list(jg["kd"])
+    rg = rot_joint_gains or GAINS_L_ROT
+    r = list(rg["kp"]) + list(rg["kd"])
     for k in range(12):
         c.task_gains[k] = g[k]
         c.joint_gains[k] = j[k]
+        c.rot_joint_gains[k] = r[k]
     c.seed = seed
     c.env_id_offset = env_id_offset
     c.envs_per_block = envs_per_block
@@ -238,4 +245,5 @@ class Batch:
 
 
 __all__ = ["Batch", "make_config", "load_model", "load_library", "TASK_GYM_V2", "TASK_TRAJ_L", "TASK_MOVE_J",
-           "TASK_CTRL", "TASK_GYM_V0", "TASK_IMIT_INDIRECT", "TASK_IMIT_DIRECT", "GAINS_L_MUG", "GAINS_V0", "GAINS_J", "np"]
+           "TASK_CTRL", "TASK_GYM_V0", "TASK_IMIT_INDIRECT", "TASK_IMIT_DIRECT", "TASK_MOVE_L", "GAINS_L_MUG", "GAINS_V0",
+           "GAINS_J", "GAINS_L_POS", "GAINS_L_ROT", "np"]
