@@ -619,8 +619,13 @@ KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
   const double* mug = s.site_xpos[sh];
   const double* gh = s.xpos[gb];
   double vt[6], vh[6];
-  w_site_velocity(m, s, st, vt);
-  w_site_velocity(m, s, sh, vh);
+  if constexpr (KS::OVERLAY) {
+    /* computed in w_forward while cvel was alive (same sites, same expression) */
+    for (int k = 0; k < 6; k++) { vt[k] = s.site_vel[0][k]; vh[k] = s.site_vel[1][k]; }
+  } else {
+    w_site_velocity(m, s, st, vt);
+    w_site_velocity(m, s, sh, vh);
+  }
   for (int k = 0; k < 3; k++) {
     obs[k] = tcp[k];
     obs[3 + k] = mug[k];
@@ -894,10 +899,12 @@ template <int NT, class KS>
 WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
                         const double* __restrict__ actions, int adim, KS& s, WOut& o) {
   const int tid = threadIdx.x;
+  WT_START();
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
   for (int k = tid; k < NCARRY; k += NT) o.carry[k] = st.carry[SC(st, k, e)];
   SYNC();
+  WT(24);
   if (tid == 0) {
     double ctrl[K_NU];
     if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L || c.task == UR3E_TASK_GYM_V0 ||
@@ -941,6 +948,15 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
   int sub = 0, retried = 0, resetting = 0;
   w_step_pre<NT>(m, s);
   for (;;) {
+    /* the model and plan are read-only kernel arguments, so their loads are invariant and LICM
+       would hoist every model constant of the forward pass out of this loop, keeping them live
+       (and spilled) across the whole substep; passing the pointers through an empty asm makes
+       them loop-variant, so each stage loads its constants where it uses them */
+    const ur3e_model_t* mi = m;
+    const KPlan* pli = pl;
+    asm volatile("" : "+s"(mi), "+s"(pli));
+#define m mi
+#define pl pli
     w_forward<NT>(m, pl, s);
     if (KS::BAIL && s.ovf) return false;
     if (resetting) {
@@ -959,6 +975,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     }
     w_make_carry<NT>(m, pl, s, o.carry);
     SYNC();
+    WT(25);
     if (!k_is_gym(c.task)) {
       if (tid == 0) {
         o.t += 1; o.ep_len += 1;
@@ -1004,6 +1021,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       o.trunc = trunc;
     }
     SYNC();
+    WT(26);
     if ((o.term || o.trunc) && c.auto_reset) {
       for (int k = tid; k < k_obs_dim(c.task); k += NT) o.tobs[k] = o.obs[k];
       if (tid == 0) o.did_reset = 1;
@@ -1013,6 +1031,8 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       continue;
     }
     return true;
+#undef m
+#undef pl
   }
 }
 
@@ -1033,8 +1053,13 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
 
 /* one env per workgroup; a compact-tier (KS::BAIL) env that overflows is queued on ovf_list
    for w_env_step_list and writes nothing */
+/* waves per SIMD the compact tier is compiled for: 2 caps it at 256 registers (arch + acc) so two
+   envs share a SIMD when LDS allows (the overlaid layout) */
+#ifndef W_COMPACT_WPE
+#define W_COMPACT_WPE 2
+#endif
 template <int NT, class KS>
-__global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+__global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                   KConfig c, KState st, const double* __restrict__ actions, int adim,
                                                   double* __restrict__ obs_out, double* __restrict__ rew_out,
                                                   unsigned char* __restrict__ term_out,
@@ -1045,11 +1070,15 @@ __global__ __launch_bounds__(NT) void w_env_step(const ur3e_model_t* __restrict_
   __shared__ WOut o;
   const int e = blockIdx.x;
   if (e >= st.n) return;
+  WT_INIT();
   if (!w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o)) {
     if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = e;
+    WT_FLUSH();
     return;
   }
   w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+  WT(27);
+  WT_FLUSH();
 }
 
 /* full-capacity tier over the envs the compact tier queued (grid-stride over the list) */
@@ -1444,57 +1473,6 @@ extern "C" int ur3e_batch_get_info(ur3e_batch_t* b, int* d_ncon, int* d_ep_len, 
   return UR3E_OK;
 }
 
-#ifdef UR3E_STAGE_TIMING
-/* diagnostic: cycles of ONE stage of the compact tier, repeated `reps` times on each env's
-   primed LDS state (w_forward once first) */
-__global__ __launch_bounds__(64) void w_stage_bench(const ur3e_model_t* __restrict__ m,
-                                                    const KPlan* __restrict__ pl, KConfig c, KState st, int stage,
-                                                    int reps, unsigned long long* __restrict__ cyc) {
-  __shared__ KSS_NV s;
-  __shared__ WOut o;
-  const int e = blockIdx.x;
-  if (e >= st.n) return;
-  w_load<64>(m, c, st, e, s, o);
-  SYNC64();
-  w_forward<64>(m, pl, s);
-  if (s.ovf) { if (threadIdx.x == 0) cyc[e] = 0; return; }
-  unsigned long long t0 = __builtin_amdgcn_s_memtime();
-  for (int r = 0; r < reps; r++) {
-    switch (stage) {
-      case 0: r_kinematics(m, pl, s); break;
-      case 1: w_com_pos<64>(m, pl, s); break;
-      case 2: w_crb<64>(m, s); break;
-      case 3: w_collision<64>(m, s); break;
-      case 4: w_make_constraint<64>(m, pl, s); break;
-      case 5: r_vel_acc(m, pl, s); break;
-      case 6: w_rne_passive<64>(m, pl, s); break;
-      case 7: { double x = r_tree_solve(m, pl, s, false, threadIdx.x < 20 ? s.qfrc_smooth[threadIdx.x] : 0.0);
-                if (threadIdx.x < 20) s.qacc_smooth[threadIdx.x] = x; SYNC64(); } break;
-      case 8: r_solve_newton(m, s); break;
-      case 9: w_forward<64>(m, pl, s); break;
-      case 10: r_kinematics<KSS_NV, 1>(m, pl, s); break;
-      case 11: r_kinematics<KSS_NV, 2>(m, pl, s); break;
-      case 12: r_kinematics<KSS_NV, 3>(m, pl, s); break;
-      case 13: w_make_constraint<64, KSS_NV, 1>(m, pl, s); break;
-      case 14: w_make_constraint<64, KSS_NV, 2>(m, pl, s); break;
-      case 15: w_make_constraint<64, KSS_NV, 3>(m, pl, s); break;
-      case 16: w_collision<64, KSS_NV, 1>(m, s); break;
-      default: break;
-    }
-  }
-  unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) cyc[e] = (t1 - t0) / (unsigned long long)(reps > 0 ? reps : 1);
-}
-
-extern "C" int ur3e_debug_stage_bench(ur3e_batch_t* b, int stage, int reps, unsigned long long* d_cycles) {
-  HIPCHK(hipSetDevice(b->device));
-  hipLaunchKernelGGL(w_stage_bench, dim3(b->n), dim3(64), 0, 0, b->d_model, b->d_plan, b->cfg, b->st, stage, reps,
-                     d_cycles);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipDeviceSynchronize());
-  return UR3E_OK;
-}
-#endif
 
 __global__ void k_env_get_carry(KState s, double* __restrict__ out) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;

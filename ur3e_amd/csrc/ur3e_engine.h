@@ -540,9 +540,8 @@ struct KRaw {
   double dist;
 };
 
-KD void k_make_frame(double f[9], const double n[3]) {
-  f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
-  k_normalize3(f);
+/* rows 1 and 2 of a contact frame whose row 0 (the unit normal) is already in f[0..2] */
+KD void k_frame_rest(double f[9]) {
   double y[3];
   if (fabs(f[1]) < 0.5) { y[0] = 0; y[1] = 1; y[2] = 0; }
   else { y[0] = 0; y[1] = 0; y[2] = 1; }
@@ -553,6 +552,12 @@ KD void k_make_frame(double f[9], const double n[3]) {
   double z[3];
   k_cross3(z, f, y);
   f[6] = z[0]; f[7] = z[1]; f[8] = z[2];
+}
+
+KD void k_make_frame(double f[9], const double n[3]) {
+  f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
+  k_normalize3(f);
+  k_frame_rest(f);
 }
 
 KD int k_plane_box(const double pp[3], const double pm[9], const double bp[3], const double bm[9],

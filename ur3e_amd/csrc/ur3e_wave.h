@@ -53,8 +53,16 @@ struct KPlan {
 #define G_LIMIT 3
 #define G_CONTACT 4
 
-template <int MC, int ME, int NVC = 0, int TREE = 0>
-struct KSX {
+/* Two LDS layouts.  The full-capacity tier (rows > 64, KSL) keeps every array side by side.  The
+   compact tier (rows <= 64: one 64-lane wavefront, register-resident solver) overlays the arrays
+   of the position/velocity stages with those of the constraint stages, see the specialisation
+   below. */
+template <int MC, int ME, int NVC = 0, int TREE = 0, bool OVERLAY = (ME <= 64)>
+struct KSX;
+
+template <int MC, int ME, int NVC, int TREE>
+struct KSX<MC, ME, NVC, TREE, false> {
+  static constexpr bool OVERLAY = false;
   static constexpr int NV = NVC;    /* > 0: kernel specialised for a model with exactly NVC dofs */
   static constexpr int STATIC_TREE = TREE; /* 1: main.xml's dof tree as compile-time tables */
   static constexpr int MAXCON = MC; /* contacts this tier holds */
@@ -106,7 +114,95 @@ struct KSX {
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
   unsigned long long tlast;
+#ifdef UR3E_STAGE_TIMING
+  unsigned long long tacc[32];
+  unsigned int tcnt[32];
+#endif
 };
+
+/* Compact-tier layout (one 64-lane wavefront per env), sized so that EIGHT envs fit the 160 KB
+   of LDS of a CU (<= 20 KB each, two wavefronts per SIMD).  w_forward runs its stages in the order
+     kinematics -> com_pos -> crb -> com_vel/RNE/passive/actuation -> collision -> constraint rows
+     -> M^-1 qfrc_smooth -> Newton -> touch -> Euler,
+   and the arrays are grouped by lifetime:
+     - outside the union: what survives a substep or is read by the epilogue / carry (state, body
+       and site positions, com quantities, packed qM, contacts, dof vectors) plus three small
+       values precomputed so that their inputs can die early: the connect-constraint anchors
+       (eq_p, from xmat), the tcp/handle site velocities (site_vel, from cvel) and the unit
+       contact normals (con_n; the rest of the contact frame is rebuilt from it, bit for bit);
+     - KC, kinematics .. collision: geom poses, collision candidates;
+     - KA, kinematics .. com_pos: body orientations, joint axes/anchors (overlaid with KB);
+     - KB, com_pos .. RNE: cinert, cvel, cdof_dot, crb/cacc/cfrc, actuation;
+     - N, constraint rows .. Euler: Jacobian and row data, cone Hessians, the packed Newton
+       Hessian / tree-factor scratch (the register solver only touches j <= i).
+   Only the fields the compact code path touches exist here. */
+#define KTRI(i, j) ((i) * ((i) + 1) / 2 + (j))
+template <int MC, int ME, int NVC, int TREE>
+struct KSX<MC, ME, NVC, TREE, true> {
+  static constexpr bool OVERLAY = true;
+  static constexpr int NV = NVC;
+  static constexpr int STATIC_TREE = TREE;
+  static constexpr int MAXCON = MC;
+  static constexpr int MAXEFC = ME;
+  static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
+  static constexpr bool BAIL = (MC < K_MAXCON) || (ME < K_MAXEFC);
+  /* ---- live for the whole env-step ---- */
+  double qpos[K_NQ], qvel[K_NV], warm[K_NV], ctrl[K_NU];
+  double xpos[K_NB][3];
+  double site_xpos[K_NS][3], site_xmat[K_NS][9];
+  double subtree_com[K_NB][3], cdof[K_NV][6];
+  double qMp[K_NV * (K_NV + 1) / 2]; /* mass matrix, packed lower triangle */
+  double qfrc_bias[K_NV], qfrc_smooth[K_NV], qacc_smooth[K_NV], qacc[K_NV], qfrc_constraint[K_NV];
+  double con_pos[MC][3], con_n[MC][3], con_dist[MC], con_mu[MC];
+  int con_geom1[MC], con_geom2[MC], con_cpair[MC], con_efc[MC];
+  double touch[UR3E_MAXTOUCH];
+  double eq_p[UR3E_MAXEQ][6];  /* connect anchors p1, p2 in world coordinates */
+  double site_vel[2][6];       /* [tcp, handle] mj_objectVelocity (world, [w, v]) */
+  int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
+  unsigned long long tlast;
+#ifdef UR3E_STAGE_TIMING
+  unsigned long long tacc[32];
+  unsigned int tcnt[32];
+#endif
+  union {
+    struct {
+      /* KC */
+      double geom_xpos[K_NG][3], geom_xmat[K_NG][9];
+      int cand_count[W_MAXCAND], cand_off[W_MAXCAND];
+      union {
+        struct { /* KA */
+          double xquat[K_NB][4], xmat[K_NB][9];
+          double xanchor[K_NJ][3], xaxis[K_NJ][3], qloc[K_NJ][4];
+        };
+        struct { /* KB */
+          double cinert[K_NB][10], cdof_dot[K_NV][6], cvel[K_NB][6];
+          double actuator_length[K_NU], act_force[K_NU], qfrc_passive[K_NV];
+          union {
+            struct {
+              double b10[K_NB][10];
+              double b6[K_NB][6];
+            } body;
+          } u;
+        };
+      };
+    };
+    struct { /* N */
+      double efc_J[ME][K_NV];
+      double efc_R[ME], efc_D[ME], efc_aref[ME], efc_force[ME];
+      int efc_type[ME], efc_id[ME], efc_grp[ME];
+      int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
+      double con_Hc[MC][9];
+      double Hl[K_NV * (K_NV + 1) / 2];
+    };
+  };
+};
+
+/* mass-matrix element (i, j) in either layout */
+template <class KS>
+__device__ __forceinline__ double qm_get(const KS& s, int i, int j) {
+  if constexpr (KS::OVERLAY) return s.qMp[i >= j ? KTRI(i, j) : KTRI(j, i)];
+  else return s.qM[i][j];
+}
 /* full-capacity tier: the oracle's limits (UR3E_MAXCON contacts, UR3E_MAXEFC rows) */
 typedef KSX<K_MAXCON, K_MAXEFC> KSL;
 /* compact tier: sized for the contact/row counts main.xml actually reaches
@@ -157,12 +253,14 @@ __device__ __forceinline__ int w_any(int pred) {
 #ifdef UR3E_STAGE_TIMING
 __device__ unsigned long long ur3e_stage_cycles[32];
 __device__ unsigned long long ur3e_stage_calls[32];
+/* accumulated per wave in LDS and flushed once at kernel end: a global atomic per mark would sit in
+   the wave's vmcnt queue and bill its (contended) latency to the next stage that loads from memory */
 #define WT(k)                                                           \
   do {                                                                  \
     if (threadIdx.x == 0) {                                             \
       unsigned long long _t = __builtin_amdgcn_s_memtime();            \
-      atomicAdd(&ur3e_stage_cycles[k], _t - s.tlast);                   \
-      atomicAdd(&ur3e_stage_calls[k], 1ull);                            \
+      s.tacc[k] += _t - s.tlast;                                        \
+      s.tcnt[k] += 1;                                                   \
       s.tlast = _t;                                                     \
     }                                                                   \
   } while (0)
@@ -170,11 +268,29 @@ __device__ unsigned long long ur3e_stage_calls[32];
   do {                                                                  \
     if (threadIdx.x == 0) s.tlast = __builtin_amdgcn_s_memtime();       \
   } while (0)
+#define WT_INIT()                                                       \
+  do {                                                                  \
+    if (threadIdx.x < 32) { s.tacc[threadIdx.x] = 0; s.tcnt[threadIdx.x] = 0; } \
+  } while (0)
+#define WT_FLUSH()                                                      \
+  do {                                                                  \
+    __builtin_amdgcn_wave_barrier();                                    \
+    if (threadIdx.x < 32 && s.tcnt[threadIdx.x]) {                      \
+      atomicAdd(&ur3e_stage_cycles[threadIdx.x], s.tacc[threadIdx.x]);  \
+      atomicAdd(&ur3e_stage_calls[threadIdx.x], (unsigned long long)s.tcnt[threadIdx.x]); \
+    }                                                                   \
+  } while (0)
 #else
 #define WT(k) \
   do {        \
   } while (0)
 #define WT_START() \
+  do {             \
+  } while (0)
+#define WT_INIT() \
+  do {            \
+  } while (0)
+#define WT_FLUSH() \
   do {             \
   } while (0)
 #endif
@@ -286,6 +402,46 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   SYNC();
+  for (int j = tid; j < m->njnt; j += NT) {
+    int b = m->jnt_bodyid[j];
+    int da = m->jnt_dofadr[j];
+    const double* c = s.subtree_com[m->body_rootid[b]];
+    double off[3] = {c[0] - s.xanchor[j][0], c[1] - s.xanchor[j][1], c[2] - s.xanchor[j][2]};
+    if (m->jnt_type[j] == UR3E_JNT_FREE) {
+      for (int k = 0; k < 3; k++) {
+        for (int r = 0; r < 6; r++) s.cdof[da + k][r] = 0;
+        s.cdof[da + k][3 + k] = 1;
+      }
+      for (int k = 0; k < 3; k++) {
+        double ax[3] = {s.xmat[b][k], s.xmat[b][3 + k], s.xmat[b][6 + k]};
+        double cr[3];
+        k_cross3(cr, ax, off);
+        s.cdof[da + 3 + k][0] = ax[0]; s.cdof[da + 3 + k][1] = ax[1]; s.cdof[da + 3 + k][2] = ax[2];
+        s.cdof[da + 3 + k][3] = cr[0]; s.cdof[da + 3 + k][4] = cr[1]; s.cdof[da + 3 + k][5] = cr[2];
+      }
+    } else {
+      double cr[3];
+      k_cross3(cr, s.xaxis[j], off);
+      s.cdof[da][0] = s.xaxis[j][0]; s.cdof[da][1] = s.xaxis[j][1]; s.cdof[da][2] = s.xaxis[j][2];
+      s.cdof[da][3] = cr[0]; s.cdof[da][4] = cr[1]; s.cdof[da][5] = cr[2];
+    }
+  }
+  if constexpr (KS::OVERLAY) {
+    /* connect anchors for the constraint rows (r_mc_rows), while xmat is still alive */
+    for (int e = tid; e < m->neq; e += NT) {
+      if (m->eq_type[e] != UR3E_EQ_CONNECT) continue;
+      const int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      double p1[3], p2[3];
+      k_mat_vec3(p1, s.xmat[b1], m->eq_data[e]);
+      p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
+      k_mat_vec3(p2, s.xmat[b2], m->eq_data[e] + 3);
+      p2[0] += s.xpos[b2][0]; p2[1] += s.xpos[b2][1]; p2[2] += s.xpos[b2][2];
+      for (int k = 0; k < 3; k++) { s.eq_p[e][k] = p1[k]; s.eq_p[e][3 + k] = p2[k]; }
+    }
+    /* xquat/xmat/xanchor/xaxis (KA) are dead from here; cinert and actuator_length (KB) reuse
+       their bytes, so every KA read above must have issued first */
+    SYNC();
+  }
   if (tid < nb) {
     int i = tid;
     double* r = s.cinert[i];
@@ -317,30 +473,6 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
       r[9] = mass;
     }
   }
-  for (int j = tid; j < m->njnt; j += NT) {
-    int b = m->jnt_bodyid[j];
-    int da = m->jnt_dofadr[j];
-    const double* c = s.subtree_com[m->body_rootid[b]];
-    double off[3] = {c[0] - s.xanchor[j][0], c[1] - s.xanchor[j][1], c[2] - s.xanchor[j][2]};
-    if (m->jnt_type[j] == UR3E_JNT_FREE) {
-      for (int k = 0; k < 3; k++) {
-        for (int r = 0; r < 6; r++) s.cdof[da + k][r] = 0;
-        s.cdof[da + k][3 + k] = 1;
-      }
-      for (int k = 0; k < 3; k++) {
-        double ax[3] = {s.xmat[b][k], s.xmat[b][3 + k], s.xmat[b][6 + k]};
-        double cr[3];
-        k_cross3(cr, ax, off);
-        s.cdof[da + 3 + k][0] = ax[0]; s.cdof[da + 3 + k][1] = ax[1]; s.cdof[da + 3 + k][2] = ax[2];
-        s.cdof[da + 3 + k][3] = cr[0]; s.cdof[da + 3 + k][4] = cr[1]; s.cdof[da + 3 + k][5] = cr[2];
-      }
-    } else {
-      double cr[3];
-      k_cross3(cr, s.xaxis[j], off);
-      s.cdof[da][0] = s.xaxis[j][0]; s.cdof[da][1] = s.xaxis[j][1]; s.cdof[da][2] = s.xaxis[j][2];
-      s.cdof[da][3] = cr[0]; s.cdof[da][4] = cr[1]; s.cdof[da][5] = cr[2];
-    }
-  }
   for (int a = tid; a < m->nu; a += NT) {
     double g = m->act_gear[a];
     if (m->act_trntype[a] == UR3E_TRN_JOINT) {
@@ -363,7 +495,11 @@ WD void w_crb(KModel m, KS& s) {
   const int tid = threadIdx.x;
   const int nb = m->nbody, nv = NVOF(KS, m);
   for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
-  for (int e = tid; e < nv * nv; e += NT) s.qM[e / nv][e % nv] = 0;
+  if constexpr (KS::OVERLAY) {
+    for (int e = tid; e < nv * (nv + 1) / 2; e += NT) s.qMp[e] = 0;
+  } else {
+    for (int e = tid; e < nv * nv; e += NT) s.qM[e / nv][e % nv] = 0;
+  }
   SYNC();
   if (tid < 10) {
     for (int i = nb - 1; i > 0; i--) {
@@ -378,12 +514,17 @@ WD void w_crb(KModel m, KS& s) {
     k_mul_inert_vec(buf, s.u.body.b10[m->dof_bodyid[i]], s.cdof[i]);
     double mii = m->dof_armature[i];
     mii += k_dot6(s.cdof[i], buf);
-    s.qM[i][i] = mii;
+    if constexpr (KS::OVERLAY) s.qMp[KTRI(i, i)] = mii;
+    else s.qM[i][i] = mii;
     for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) {
       double v = 0.0;
       v += k_dot6(s.cdof[j], buf);
-      s.qM[i][j] = v;
-      s.qM[j][i] = v;
+      if constexpr (KS::OVERLAY) {
+        s.qMp[KTRI(i, j)] = v; /* ancestors have lower indices */
+      } else {
+        s.qM[i][j] = v;
+        s.qM[j][i] = v;
+      }
     }
   }
   SYNC();
@@ -491,7 +632,13 @@ WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
 template <class KS>
 WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
   s.con_pos[c][0] = r.pos[0]; s.con_pos[c][1] = r.pos[1]; s.con_pos[c][2] = r.pos[2];
-  k_make_frame(s.con_frame[c], r.n);
+  if constexpr (KS::OVERLAY) {
+    double u[3] = {r.n[0], r.n[1], r.n[2]};
+    k_normalize3(u); /* = frame row 0 of k_make_frame */
+    s.con_n[c][0] = u[0]; s.con_n[c][1] = u[1]; s.con_n[c][2] = u[2];
+  } else {
+    k_make_frame(s.con_frame[c], r.n);
+  }
   s.con_dist[c] = r.dist;
   s.con_geom1[c] = m->cpair_geom1[p];
   s.con_geom2[c] = m->cpair_geom2[p];
@@ -1431,7 +1578,8 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = threadIdx.x;
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64); /* compact tier: ur3e_wave_r.h */
-  WT_START();
+  static_assert(!KS::OVERLAY || REG, "the overlaid layout is only valid for the 64-lane register path");
+  WT(23);
   if constexpr (REG) {
     if (pl->max_jntnum <= 1) r_kinematics(m, pl, s);
     else w_kinematics<NT>(m, pl, s);
@@ -1449,17 +1597,33 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
     w_factor_tree<NT>(m, pl, s.H, s.LDinv, s.tmpv);
   }
   WT(3);
+  if constexpr (KS::OVERLAY) {
+    /* velocity-dependent forces first: their scratch shares bytes with the constraint rows */
+    r_vel_acc(m, pl, s);
+    /* the epilogue's site velocities (w_obs_v2), while cvel (KB) is alive */
+    if (tid < 2) {
+      const int site = tid == 0 ? m->id_site_tcp : m->id_site_handle;
+      double v[6] = {0, 0, 0, 0, 0, 0};
+      if (site >= 0) w_site_velocity(m, s, site, v);
+      for (int k = 0; k < 6; k++) s.site_vel[tid][k] = v[k];
+    }
+    WT(6);
+    w_rne_passive<NT>(m, pl, s);
+    WT(7);
+  }
   w_collision<NT>(m, s);
   WT(4);
   if (KS::BAIL && s.ovf) return;
   w_make_constraint<NT>(m, pl, s);
   WT(5);
   if (KS::BAIL && s.ovf) return;
-  if constexpr (REG) r_vel_acc(m, pl, s);
-  else w_com_vel<NT>(m, pl, s);
-  WT(6);
-  w_rne_passive<NT>(m, pl, s);
-  WT(7);
+  if constexpr (!KS::OVERLAY) {
+    if constexpr (REG) r_vel_acc(m, pl, s);
+    else w_com_vel<NT>(m, pl, s);
+    WT(6);
+    w_rne_passive<NT>(m, pl, s);
+    WT(7);
+  }
   if constexpr (REG) {
     double x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0);
     if (tid < nv) s.qacc_smooth[tid] = x;
@@ -1491,7 +1655,9 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
           double sp[3], sm[9], ss[3];
           for (int k = 0; k < 3; k++) { sp[k] = s.site_xpos[site][k]; ss[k] = m->site_size[site][k]; }
           for (int k = 0; k < 9; k++) sm[k] = s.site_xmat[site][k];
-          double ray[3] = {s.con_frame[ci][0], s.con_frame[ci][1], s.con_frame[ci][2]};
+          double ray[3];
+          if constexpr (KS::OVERLAY) { ray[0] = s.con_n[ci][0]; ray[1] = s.con_n[ci][1]; ray[2] = s.con_n[ci][2]; }
+          else { ray[0] = s.con_frame[ci][0]; ray[1] = s.con_frame[ci][1]; ray[2] = s.con_frame[ci][2]; }
           if (body == b2) { ray[0] = -ray[0]; ray[1] = -ray[1]; ray[2] = -ray[2]; }
           double cp[3] = {s.con_pos[ci][0], s.con_pos[ci][1], s.con_pos[ci][2]};
           if (k_ray_box_hit(sp, sm, ss, cp, ray)) val = fn;
@@ -1506,6 +1672,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
       if (tid == k) mine = sum;
     }
     if (tid < nt) s.touch[tid] = mine;
+    WT(21);
   } else if (tid < m->ntouch) {
     const int site = m->touch_site[tid];
     const int body = m->site_bodyid[site];
@@ -1520,7 +1687,9 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
       if (body != b1 && body != b2) continue;
       const double fn = s.efc_force[adr];
       if (fn <= 0) continue;
-      double ray[3] = {s.con_frame[ci][0], s.con_frame[ci][1], s.con_frame[ci][2]};
+      double ray[3];
+      if constexpr (KS::OVERLAY) { ray[0] = s.con_n[ci][0]; ray[1] = s.con_n[ci][1]; ray[2] = s.con_n[ci][2]; }
+      else { ray[0] = s.con_frame[ci][0]; ray[1] = s.con_frame[ci][1]; ray[2] = s.con_frame[ci][2]; }
       if (body == b2) { ray[0] = -ray[0]; ray[1] = -ray[1]; ray[2] = -ray[2]; }
       double cp[3] = {s.con_pos[ci][0], s.con_pos[ci][1], s.con_pos[ci][2]};
       if (k_ray_box_hit(sp, sm, ss, cp, ray)) sum += fn;
@@ -1564,35 +1733,10 @@ WD int w_step_badacc(KModel m, KS& s) {
   return 0;
 }
 
+/* mj_Euler's position update (free joints: quaternion integration) */
 template <int NT, class KS>
-WD void w_step_euler(KModel m, const KPlan* __restrict__ pl, KS& s) {
+WD void w_integrate_pos(KModel m, KS& s, double h) {
   const int tid = threadIdx.x;
-  const int nv = NVOF(KS, m);
-  /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
-  int damped = 0;
-  for (int k = 0; k < nv; k++) damped |= m->dof_damping[k] > 0;
-  if (!damped) {
-    if (tid < nv) s.xv[tid] = s.qacc[tid];
-    SYNC();
-  } else if constexpr (NT == 64 && KS::MAXEFC <= 64) {
-    double x = r_tree_solve(m, pl, s, true, tid < nv ? s.qfrc_smooth[tid] + s.qfrc_constraint[tid] : 0.0);
-    if (tid < nv) s.xv[tid] = x;
-    SYNC();
-  } else {
-    for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
-    SYNC();
-    if (tid < nv) {
-      s.H[tid][tid] += m->timestep * m->dof_damping[tid];
-      s.fv[tid] = s.qfrc_smooth[tid] + s.qfrc_constraint[tid];
-    }
-    SYNC();
-    w_factor_tree<NT>(m, pl, s.H, s.grad, s.tmpv);
-    w_solve_tree<NT>(m, pl, s.H, s.grad, s.xv, s.fv);
-  }
-  WT(16);
-  double h = m->timestep;
-  if (tid < nv) s.qvel[tid] += h * s.xv[tid];
-  SYNC();
   for (int j = tid; j < m->njnt; j += NT) {
     int a = m->jnt_qposadr[j], v = m->jnt_dofadr[j];
     if (m->jnt_type[j] == UR3E_JNT_FREE) {
@@ -1611,6 +1755,47 @@ WD void w_step_euler(KModel m, const KPlan* __restrict__ pl, KS& s) {
       s.qpos[a] += h * s.qvel[v];
     }
   }
+}
+
+template <int NT, class KS>
+WD void w_step_euler(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  const int tid = threadIdx.x;
+  const int nv = NVOF(KS, m);
+  /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
+  WT(22);
+  int damped = 0;
+  for (int k = 0; k < nv; k++) damped |= m->dof_damping[k] > 0;
+  double x = 0; /* qacc used for the velocity update, lane = dof */
+  if constexpr (KS::OVERLAY) {
+    /* the solve's result stays in the lane's register (no LDS vector) */
+    if (!damped) x = tid < nv ? s.qacc[tid] : 0.0;
+    else x = r_tree_solve(m, pl, s, true, tid < nv ? s.qfrc_smooth[tid] + s.qfrc_constraint[tid] : 0.0);
+  } else {
+    if (!damped) {
+      if (tid < nv) s.xv[tid] = s.qacc[tid];
+      SYNC();
+    } else if constexpr (NT == 64 && KS::MAXEFC <= 64) {
+      double y = r_tree_solve(m, pl, s, true, tid < nv ? s.qfrc_smooth[tid] + s.qfrc_constraint[tid] : 0.0);
+      if (tid < nv) s.xv[tid] = y;
+      SYNC();
+    } else {
+      for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
+      SYNC();
+      if (tid < nv) {
+        s.H[tid][tid] += m->timestep * m->dof_damping[tid];
+        s.fv[tid] = s.qfrc_smooth[tid] + s.qfrc_constraint[tid];
+      }
+      SYNC();
+      w_factor_tree<NT>(m, pl, s.H, s.grad, s.tmpv);
+      w_solve_tree<NT>(m, pl, s.H, s.grad, s.xv, s.fv);
+    }
+    if (tid < nv) x = s.xv[tid];
+  }
+  WT(16);
+  double h = m->timestep;
+  if (tid < nv) s.qvel[tid] += h * x;
+  SYNC();
+  w_integrate_pos<NT>(m, s, h);
   if (tid < nv) s.warm[tid] = s.qacc[tid];
   SYNC();
   WT(17);

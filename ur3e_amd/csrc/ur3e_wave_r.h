@@ -42,8 +42,7 @@ __device__ __forceinline__ int shfi(int v, int src) { return __builtin_amdgcn_ds
 struct RRow {
   int typ, jj, first; /* jj: row index inside its contact, first: lane of the contact's first row */
   double D, R, aref, floss, mu, fr0, fr1;
-  double J[K_NV];
-  double jar, Jv, force, F;
+  double jar, Jv, force, F; /* the Jacobian row stays in LDS (efc_J): 40 fewer live registers */
   int st, flag;
 };
 
@@ -54,13 +53,11 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w) {
   w.typ = -1; w.jj = 0; w.first = r;
   w.D = 0; w.R = 0; w.aref = 0; w.floss = 0; w.mu = 0; w.fr0 = 0; w.fr1 = 0;
   w.jar = 0; w.Jv = 0; w.force = 0; w.F = 0; w.st = ST_SATISFIED; w.flag = 0;
-#pragma unroll
-  for (int k = 0; k < K_NV; k++) w.J[k] = 0;
   if (r < nefc) {
     w.typ = s.efc_type[r];
-    w.D = s.efc_D[r]; w.R = s.efc_R[r]; w.aref = s.efc_aref[r]; w.floss = s.efc_floss[r];
-#pragma unroll
-    for (int k = 0; k < K_NV; k++) w.J[k] = s.efc_J[r][k];
+    w.D = s.efc_D[r]; w.R = s.efc_R[r]; w.aref = s.efc_aref[r];
+    /* frictionloss rows: efc_id is the dof (r_mc_layout) */
+    w.floss = w.typ == CN_FRICTION_DOF ? m->dof_frictionloss[s.efc_id[r]] : 0.0;
     if (w.typ != CN_EQUALITY && w.typ != CN_FRICTION_DOF && w.typ != CN_LIMIT_JOINT) {
       int c = s.efc_id[r];
       int i0 = s.con_efc[c];
@@ -145,6 +142,19 @@ WD void r_constraint_update(RRow& w) {
   }
 }
 
+/* J[lane] . x in dof order, the row read from LDS (lanes >= nefc: a zero row, as the oracle's
+   unused rows never enter a sum; +0 + 0*x stays +0) */
+template <class KS>
+WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV]) {
+  const bool act = (int)threadIdx.x < nefc;
+  const int r = act ? threadIdx.x : 0;
+  double v = 0;
+#pragma unroll
+  for (int k = 0; k < K_NV; k++)
+    if (k < nv) v += (act ? s.efc_J[r][k] : 0.0) * x[k];
+  return v;
+}
+
 /* uniform copy of a dof vector held one element per lane */
 WD void r_bcast(double v, int nv, double out[K_NV]) {
 #pragma unroll
@@ -164,16 +174,10 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
     const int row = lane < nv ? lane : 0;
 #pragma unroll
     for (int j = 0; j < K_NV; j++)
-      if (j < nv) v += s.qM[row][j] * qv[j];
+      if (j < nv) v += qm_get(s, row, j) * qv[j];
     Ma = v;
   }
-  {
-    double v = 0;
-#pragma unroll
-    for (int k = 0; k < K_NV; k++)
-      if (k < nv) v += w.J[k] * qv[k];
-    w.jar = v - w.aref;
-  }
+  w.jar = r_row_dot(s, nv, nefc, qv) - w.aref;
   r_constraint_update(w);
   double term = (Ma - qs) * (qacc - qas);
   double a0 = 0, a1 = 0;
@@ -195,11 +199,10 @@ WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double q
   const int nefc = s.nefc;
   const int col = lane < K_NV ? lane : 0;
   double f = 0;
-#pragma unroll
-  for (int i = 0; i < KS::MAXEFC; i++) {
-    double n = f + s.efc_J[i][col] * rl(w.force, i);
-    f = i < nefc ? n : f;
-  }
+  /* partially unrolled: a fully unrolled MAXEFC-row loop hoists every J load and force
+     broadcast at once (88 live VGPRs) */
+#pragma unroll 4
+  for (int i = 0; i < nefc; i++) f = f + s.efc_J[i][col] * rl(w.force, i);
   qfrc_c = f;
   grad = Ma - qs - f;
 }
@@ -261,7 +264,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
     if (!ev[q]) k = 0;
     ek[q] = k;
     ec[q] = ev[q] ? e - k * (k + 1) / 2 : 0;
-    hv[q] = s.qM[ek[q]][ec[q]];
+    hv[q] = s.qMp[ev[q] ? e : 0]; /* element e of the packed lower triangle is (ek, ec) */
   }
   /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
      compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
@@ -305,27 +308,28 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
       }
     }
   }
+  /* element e = lane + 64 q is packed-triangle index e */
 #pragma unroll
   for (int q = 0; q < NQ; q++)
-    if (ev[q]) s.H[ek[q]][ec[q]] = hv[q];
+    if (ev[q]) s.Hl[lane + 64 * q] = hv[q];
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   double h[K_NV];
 #pragma unroll
-  for (int c = 0; c < K_NV; c++) h[c] = c <= row ? s.H[row][c] : 0.0;
+  for (int c = 0; c < K_NV; c++) h[c] = c <= row ? s.Hl[KTRI(row, c)] : 0.0;
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   WT(10);
   /* right-looking Cholesky, lane = row; element (i,k) gets -= L[i][j] L[k][j] for j = 0,1,...
      (the oracle's left-looking order) */
-  double diag[K_NV];
+  /* L[j][j] ends on lane j (h[j]); the solves read it back by readlane instead of keeping a
+     per-lane copy of the whole diagonal */
 #pragma unroll
   for (int j = 0; j < K_NV; j++) {
     if (j < nv) {
       double sum = rl(h[j], j);
       if (sum < K_MINVAL) sum = K_MINVAL;
       double ljj = sqrt(sum);
-      diag[j] = ljj;
       if (lane > j) h[j] = h[j] / ljj;
       if (lane == j) h[j] = ljj;
 #pragma unroll
@@ -343,27 +347,28 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 #pragma unroll
   for (int k = 0; k < K_NV; k++) {
     if (k < nv) {
-      double xk = rl(tmp, k) / diag[k];
+      double xk = rl(tmp, k) / rl(h[k], k);
       if (lane == k) tmp = xk;
       else if (lane > k) tmp -= h[k] * xk;
     }
   }
   WT(18);
-  /* L^T via LDS (H storage; nothing else reads it during the solve) */
+  /* L^T via LDS (packed lower triangle; nothing else reads it during the solve) */
   if (lane < nv) {
 #pragma unroll
-    for (int c = 0; c < K_NV; c++) s.H[lane][c] = h[c];
+    for (int c = 0; c < K_NV; c++)
+      if (c <= lane) s.Hl[KTRI(lane, c)] = h[c];
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   double lt[K_NV];
 #pragma unroll
-  for (int i = 0; i < K_NV; i++) lt[i] = s.H[i][row];
+  for (int i = 0; i < K_NV; i++) lt[i] = i >= row ? s.Hl[KTRI(i, row)] : 0.0;
   /* backward: L' x = y (x[i] = tmp[i] / L[i][i]; tmp[t] -= L[i][t] x[i], t < i) */
 #pragma unroll
   for (int i = K_NV - 1; i >= 0; i--) {
     if (i < nv) {
-      double xi = rl(tmp, i) / diag[i];
+      double xi = rl(tmp, i) / rl(lt[i], i);
       if (lane == i) tmp = xi;
       else if (lane < i) tmp -= lt[i] * xi;
     }
@@ -459,16 +464,10 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
     const int row = lane < nv ? lane : 0;
 #pragma unroll
     for (int j = 0; j < K_NV; j++)
-      if (j < nv) v += s.qM[row][j] * sv[j];
+      if (j < nv) v += qm_get(s, row, j) * sv[j];
     Mv = v;
   }
-  {
-    double v = 0;
-#pragma unroll
-    for (int k = 0; k < K_NV; k++)
-      if (k < nv) v += w.J[k] * sv[k];
-    w.Jv = v;
-  }
+  w.Jv = r_row_dot(s, nv, nefc, sv);
   if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
   double g1 = 0, g2 = 0;
@@ -586,7 +585,7 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
     amask[k] = KS::STATIC_TREE ? (k < UR3E_MAIN_NV ? ur3e_main_dof_anc_mask[k] : 0u) : pl->dof_anc_mask[k];
   double a[K_NV];
 #pragma unroll
-  for (int i = 0; i < K_NV; i++) a[i] = s.qM[i][col];
+  for (int i = 0; i < K_NV; i++) a[i] = qm_get(s, i, col);
   if (damped) {
     const double hstep = m->timestep;
     const double dmp = lane < nv ? m->dof_damping[col] : 0.0;
@@ -633,16 +632,18 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
     }
   }
   if (lane < nv) x *= dinv;
+  /* column -> row hand-off through the packed lower triangle (ancestors have lower indices) */
   if (lane < nv) {
 #pragma unroll
-    for (int i = 0; i < K_NV; i++) s.H[i][lane] = a[i];
+    for (int i = 0; i < K_NV; i++)
+      if (i >= lane) s.Hl[KTRI(i, lane)] = a[i];
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   const unsigned int myam = lane < nv ? pl->dof_anc_mask[lane] : 0u;
   double r[K_NV];
 #pragma unroll
-  for (int j = 0; j < K_NV; j++) r[j] = s.H[col][j];
+  for (int j = 0; j < K_NV; j++) r[j] = j <= col ? s.Hl[KTRI(col, j)] : 0.0;
 #pragma unroll
   for (int j = 0; j < K_NV; j++) {
     if (j < nv) {
@@ -929,9 +930,8 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
     const int ct = type == G_CONNECT || type == G_JOINTEQ ? CN_EQUALITY
                  : type == G_FLOSS ? CN_FRICTION_DOF : type == G_LIMIT ? CN_LIMIT_JOINT : CN_CONTACT_ELLIPTIC;
     const int cid = type == G_LIMIT ? (id >> 1) : id;
-    const double fl = type == G_FLOSS ? m->dof_frictionloss[id] : 0.0;
     for (int k = 0; k < n; k++) {
-      s.efc_type[r + k] = ct; s.efc_id[r + k] = cid; s.efc_grp[r + k] = g; s.efc_floss[r + k] = fl;
+      s.efc_type[r + k] = ct; s.efc_id[r + k] = cid; s.efc_grp[r + k] = g;
     }
     if (type == G_CONTACT) s.con_efc[id] = r;
   };
@@ -972,14 +972,9 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (gtype == G_CONNECT) {
       const int e = id;
       const int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
-      double xm1[9], xm2[9], ed1[3], ed2[3];
-      for (int k = 0; k < 9; k++) { xm1[k] = s.xmat[b1][k]; xm2[k] = s.xmat[b2][k]; }
-      for (int k = 0; k < 3; k++) { ed1[k] = m->eq_data[e][k]; ed2[k] = m->eq_data[e][3 + k]; }
+      /* anchors precomputed in w_com_pos (xmat is dead by now) */
       double p1[3], p2[3];
-      k_mat_vec3(p1, xm1, ed1);
-      p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
-      k_mat_vec3(p2, xm2, ed2);
-      p2[0] += s.xpos[b2][0]; p2[1] += s.xpos[b2][1]; p2[2] += s.xpos[b2][2];
+      for (int k = 0; k < 3; k++) { p1[k] = s.eq_p[e][k]; p2[k] = s.eq_p[e][3 + k]; }
       const int r1 = m->body_rootid[b1], r2 = m->body_rootid[b2];
       for (int k = 0; k < 3; k++) {
         o1[k] = p1[k] - s.subtree_com[r1][k];
@@ -1037,7 +1032,8 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
         o1[k] = pk - s.subtree_com[r1][k];
         o2[k] = pk - s.subtree_com[r2][k];
       }
-      for (int k = 0; k < 9; k++) fr[k] = s.con_frame[c][k];
+      for (int k = 0; k < 3; k++) fr[k] = s.con_n[c][k];
+      k_frame_rest(fr); /* k_make_frame's rows 1-2 from the stored unit normal */
       msk1 = pl->body_dof_mask[b1]; msk2 = pl->body_dof_mask[b2];
       const double d = s.con_dist[c];
       gpos[0] = d; gpos[1] = d; gpos[2] = d;
