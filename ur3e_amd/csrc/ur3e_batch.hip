@@ -567,7 +567,7 @@ __global__ __launch_bounds__(64) void k_env_set_state(const ur3e_model_t* __rest
 /* carry from the LDS working set: tcp pose, arm Jacobian (6x6), qfrc_bias[0:6] */
 template <int NT, class KS>
 WD void w_make_carry(KModel m, const KPlan* __restrict__ pl, const KS& s, double* carry) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   int st = m->id_site_tcp;
   if (st < 0) {
     for (int k = tid; k < NCARRY; k += NT) carry[k] = 0;
@@ -810,7 +810,7 @@ struct WOut {
 
 template <int NT, class KS>
 WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut& o) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = st.qpos[SQ(st, k, e)];
   for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = st.qvel[SV(st, k, e)]; s.warm[k] = st.warm[SV(st, k, e)]; }
   if (tid == 0) {
@@ -826,7 +826,7 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
 template <int NT, class KS>
 WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& s, const WOut& o, double* obs_out,
                  double* rew_out, unsigned char* term_out, unsigned char* trunc_out, double* tobs_out, int stepped) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
@@ -853,7 +853,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
 /* reset the env held in LDS: keyframe (+ mug noise) -> forward -> obs, carry (all lanes) */
 template <int NT, class KS>
 WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   for (int k = tid; k < m->nq; k += NT) s.qpos[k] = c.reset_key >= 0 ? m->key_qpos[c.reset_key][k] : m->qpos0[k];
   for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = c.reset_key >= 0 ? m->key_qvel[c.reset_key][k] : 0.0; s.warm[k] = 0; }
   for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
@@ -880,7 +880,7 @@ WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
 
 template <int NT, class KS>
 WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c, KS& s, WOut& o) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   if (tid == 0 && (k_is_gym(c.task) || c.obs_sites)) w_task_obs(m, s, c.task, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
@@ -898,7 +898,7 @@ WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, in
 template <int NT, class KS>
 WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
                         const double* __restrict__ actions, int adim, KS& s, WOut& o) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   WT_START();
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];

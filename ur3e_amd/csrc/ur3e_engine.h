@@ -56,6 +56,15 @@
 
 #define KD __device__ static inline
 #define KDN __device__ static __attribute__((noinline))
+/* this lane's index within the workgroup, opaque to the optimiser: a value derived from
+   threadIdx.x alone is loop-invariant, and LICM would hoist all of them out of the per-substep
+   loop and keep them live (spilled) across the whole forward pass; reading the lane through an
+   empty asm makes each stage derive its lane constants where it uses them */
+__device__ __forceinline__ int w_lane() {
+  int l = (int)threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
 
 typedef const ur3e_model_t* __restrict__ KModel;
 

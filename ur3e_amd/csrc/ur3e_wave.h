@@ -257,7 +257,7 @@ __device__ unsigned long long ur3e_stage_calls[32];
    the wave's vmcnt queue and bill its (contended) latency to the next stage that loads from memory */
 #define WT(k)                                                           \
   do {                                                                  \
-    if (threadIdx.x == 0) {                                             \
+    if (w_lane() == 0) {                                             \
       unsigned long long _t = __builtin_amdgcn_s_memtime();            \
       s.tacc[k] += _t - s.tlast;                                        \
       s.tcnt[k] += 1;                                                   \
@@ -266,18 +266,18 @@ __device__ unsigned long long ur3e_stage_calls[32];
   } while (0)
 #define WT_START()                                                      \
   do {                                                                  \
-    if (threadIdx.x == 0) s.tlast = __builtin_amdgcn_s_memtime();       \
+    if (w_lane() == 0) s.tlast = __builtin_amdgcn_s_memtime();       \
   } while (0)
 #define WT_INIT()                                                       \
   do {                                                                  \
-    if (threadIdx.x < 32) { s.tacc[threadIdx.x] = 0; s.tcnt[threadIdx.x] = 0; } \
+    if (w_lane() < 32) { s.tacc[w_lane()] = 0; s.tcnt[w_lane()] = 0; } \
   } while (0)
 #define WT_FLUSH()                                                      \
   do {                                                                  \
     __builtin_amdgcn_wave_barrier();                                    \
-    if (threadIdx.x < 32 && s.tcnt[threadIdx.x]) {                      \
-      atomicAdd(&ur3e_stage_cycles[threadIdx.x], s.tacc[threadIdx.x]);  \
-      atomicAdd(&ur3e_stage_calls[threadIdx.x], (unsigned long long)s.tcnt[threadIdx.x]); \
+    if (w_lane() < 32 && s.tcnt[w_lane()]) {                      \
+      atomicAdd(&ur3e_stage_cycles[w_lane()], s.tacc[w_lane()]);  \
+      atomicAdd(&ur3e_stage_calls[w_lane()], (unsigned long long)s.tcnt[w_lane()]); \
     }                                                                   \
   } while (0)
 #else
@@ -302,7 +302,7 @@ __device__ unsigned long long ur3e_stage_calls[32];
 /* ================================================================== */
 template <int NT, class KS>
 WD void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   if (tid == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
@@ -373,7 +373,7 @@ WD void w_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
 /* ================================================================== */
 template <int NT, class KS>
 WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nb = m->nbody;
   double xipos[3] = {0, 0, 0}, ximat[9];
   if (tid < nb) {
@@ -492,7 +492,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
 /* ================================================================== */
 template <int NT, class KS>
 WD void w_crb(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nb = m->nbody, nv = NVOF(KS, m);
   for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
   if constexpr (KS::OVERLAY) {
@@ -534,7 +534,7 @@ WD void w_crb(KModel m, KS& s) {
 template <int NT>
 WD void w_factor_tree(KModel m, const KPlan* __restrict__ pl, double (*A)[K_NV], double* diaginv,
                                      double* tmp) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = m->nv;
   for (int k = nv - 1; k >= 0; k--) {
     const int na = pl->dof_nanc[k];
@@ -567,7 +567,7 @@ WD void w_factor_tree(KModel m, const KPlan* __restrict__ pl, double (*A)[K_NV],
 template <int NT>
 WD void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K_NV],
                                     const double* diaginv, double* x, const double* b) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = m->nv;
   if (tid < nv) x[tid] = b[tid];
   SYNC();
@@ -653,7 +653,7 @@ WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
    Same contacts in the same order as the count / prefix / write passes of w_collision. */
 template <class KS, int VAR = 0>
 WD void r_collision(KModel m, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int np = m->ncpair;
   int nsurv = 0;
   for (int base = 0; base < np; base += 64) {
@@ -703,7 +703,7 @@ WD void w_collision(KModel m, KS& s) {
     r_collision<KS, VAR>(m, s);
     return;
   }
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int np = m->ncpair;
   KRaw raw[8];
   for (int p = tid; p < np; p += NT) s.cand_count[p] = w_narrow(m, s, p, raw);
@@ -780,7 +780,7 @@ KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double
 
 template <int NT, class KS, int VAR = 0>
 WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64);
   if constexpr (REG) {
@@ -969,7 +969,7 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
 /* ================================================================== */
 template <int NT, class KS>
 WD void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nb = m->nbody;
   if (tid < 6) s.cvel[0][tid] = 0;
   SYNC();
@@ -1008,7 +1008,7 @@ WD void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
 
 template <int NT, class KS>
 WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nb = m->nbody, nv = NVOF(KS, m);
   double (*cacc)[10] = s.u.body.b10;
   double (*cfrc)[6] = s.u.body.b6;
@@ -1122,7 +1122,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
 /* per-row force/state and cost contribution (rowflag: adds to the cost) */
 template <int NT, class KS>
 WD void w_constraint_update(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nefc = s.nefc;
   for (int i = tid; i < nefc; i += NT) {
     int t = s.efc_type[i];
@@ -1202,7 +1202,7 @@ WD void w_constraint_update(KModel m, KS& s) {
 
 template <int NT, class KS>
 WD void w_eval_state(KModel m, KS& s, const double* qacc) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   for (int i = tid; i < nv + s.nefc; i += NT) {
     if (i < nv) {
@@ -1239,7 +1239,7 @@ WD void w_eval_state(KModel m, KS& s, const double* qacc) {
 
 template <int NT, class KS>
 WD void w_compute_grad(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   if (tid < nv) {
     int k = tid;
@@ -1253,7 +1253,7 @@ WD void w_compute_grad(KModel m, KS& s) {
 
 template <int NT, class KS>
 WD void w_hessian_factor(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   /* cone Hessians (middle zone), one lane per contact */
   for (int c = tid; c < s.ncon; c += NT) {
@@ -1347,7 +1347,7 @@ WD void w_hessian_factor(KModel m, KS& s) {
 /* x = H^-1 b by column sweeps (oracle order: forward k ascending, back k descending) */
 template <int NT, class KS>
 WD void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   if (tid < nv) s.tmpv[tid] = b[tid];
   SYNC();
@@ -1370,7 +1370,7 @@ WD void w_hessian_solve(KModel m, KS& s, double* x, const double* b) {
 /* line-search 1-D evaluation at step a: per-row contributions + ordered sums on lane 0 */
 template <int NT, class KS>
 WD void w_ls_eval(KModel m, KS& s, double a) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nefc = s.nefc;
   for (int i = tid; i < nefc; i += NT) {
     int t = s.efc_type[i];
@@ -1452,7 +1452,7 @@ WD void w_ls_eval(KModel m, KS& s, double a) {
 
 template <int NT, class KS>
 WD double w_line_search(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   if (tid == 0) {
     double sn = 0;
@@ -1514,7 +1514,7 @@ WD double w_line_search(KModel m, KS& s) {
 
 template <int NT, class KS>
 WD void w_solve_newton(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   if (s.nefc == 0) {
     if (tid < nv) { s.qacc[tid] = s.qacc_smooth[tid]; s.qfrc_constraint[tid] = 0; }
@@ -1575,7 +1575,7 @@ WD void w_solve_newton(KModel m, KS& s) {
 /* ================================================================== */
 template <int NT, class KS>
 WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64); /* compact tier: ur3e_wave_r.h */
   static_assert(!KS::OVERLAY || REG, "the overlaid layout is only valid for the 64-lane register path");
@@ -1703,7 +1703,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
    (the kernel is large; a single copy keeps its instruction footprint down) */
 template <int NT, class KS>
 WD void w_step_pre(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nq = m->nq, nv = NVOF(KS, m);
   int bad = 0;
   for (int k = tid; k < nq; k += NT) bad |= k_is_bad(s.qpos[k]);
@@ -1719,7 +1719,7 @@ WD void w_step_pre(KModel m, KS& s) {
 /* after the first forward of a substep: bad qacc -> reset state, returns 1 (forward again) */
 template <int NT, class KS>
 WD int w_step_badacc(KModel m, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nq = m->nq, nv = NVOF(KS, m);
   int bad = 0;
   for (int k = tid; k < nv; k += NT) bad |= k_is_bad(s.qacc[k]);
@@ -1736,7 +1736,7 @@ WD int w_step_badacc(KModel m, KS& s) {
 /* mj_Euler's position update (free joints: quaternion integration) */
 template <int NT, class KS>
 WD void w_integrate_pos(KModel m, KS& s, double h) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   for (int j = tid; j < m->njnt; j += NT) {
     int a = m->jnt_qposadr[j], v = m->jnt_dofadr[j];
     if (m->jnt_type[j] == UR3E_JNT_FREE) {
@@ -1759,7 +1759,7 @@ WD void w_integrate_pos(KModel m, KS& s, double h) {
 
 template <int NT, class KS>
 WD void w_step_euler(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int tid = threadIdx.x;
+  const int tid = w_lane();
   const int nv = NVOF(KS, m);
   /* Euler with implicit damping: (M + h D) qacc_int = qfrc_smooth + qfrc_constraint */
   WT(22);

@@ -48,7 +48,7 @@ struct RRow {
 
 template <class KS>
 WD void r_load_rows(KModel m, const KS& s, RRow& w) {
-  const int r = threadIdx.x;
+  const int r = w_lane();
   const int nefc = s.nefc;
   w.typ = -1; w.jj = 0; w.first = r;
   w.D = 0; w.R = 0; w.aref = 0; w.floss = 0; w.mu = 0; w.fr0 = 0; w.fr1 = 0;
@@ -74,7 +74,7 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w) {
 WD void r_constraint_update(RRow& w) {
   const double jar = w.jar, D = w.D, R = w.R;
   /* contact cone: computed on every lane (uniform shuffles), used by contact lanes */
-  double jar1 = shf(jar, threadIdx.x + 1), jar2 = shf(jar, threadIdx.x + 2);
+  double jar1 = shf(jar, w_lane() + 1), jar2 = shf(jar, w_lane() + 2);
   double mu = w.mu;
   double U0 = jar * mu, U1 = jar1 * w.fr0, U2 = jar2 * w.fr1;
   double N = U0;
@@ -146,8 +146,8 @@ WD void r_constraint_update(RRow& w) {
    unused rows never enter a sum; +0 + 0*x stays +0) */
 template <class KS>
 WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV]) {
-  const bool act = (int)threadIdx.x < nefc;
-  const int r = act ? threadIdx.x : 0;
+  const bool act = w_lane() < nefc;
+  const int r = act ? w_lane() : 0;
   double v = 0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++)
@@ -165,7 +165,7 @@ WD void r_bcast(double v, int nv, double out[K_NV]) {
 template <class KS>
 WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
                      double& cost) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double qv[K_NV];
   r_bcast(qacc, nv, qv);
@@ -195,7 +195,7 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
 /* w_compute_grad: lane k: qfrc_constraint[k] = sum_i J[i][k] force[i] (row order), grad */
 template <class KS>
 WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double qs, double& qfrc_c, double& grad) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nefc = s.nefc;
   const int col = lane < K_NV ? lane : 0;
   double f = 0;
@@ -211,7 +211,7 @@ WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double q
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
 template <class KS>
 WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   /* cone Hessians (w_hessian_factor), on each contact's first-row lane */
   {
@@ -382,7 +382,7 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 template <int ME>
 WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF, double& lsdF,
                   double& lsd2F) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const double D = w.D, R = w.R;
   double x = w.jar + a * w.Jv;
   double v = w.Jv;
@@ -449,7 +449,7 @@ WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, do
 template <class KS>
 WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, double qs, double gauss,
                         double scale) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double sv[K_NV];
   r_bcast(search, nv, sv);
@@ -514,7 +514,7 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
 /* w_solve_newton for the compact tier; leaves s.qacc and s.qfrc_constraint */
 template <class KS>
 WD void r_solve_newton(KModel m, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m);
   if (s.nefc == 0) {
     if (lane < nv) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_constraint[lane] = 0; }
@@ -575,7 +575,7 @@ WD void r_solve_newton(KModel m, KS& s) {
    w_factor_tree / w_solve_tree.  Returns x = A^-1 b on lane t (< nv). */
 template <class KS>
 WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool damped, double b) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m);
   const int col = lane < nv ? lane : 0;
   /* plan masks and damping up front: one batch of scalar loads, not one wait per column */
@@ -666,7 +666,7 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
 /* w_kinematics (mj_kinematics); VAR != 0 only in the diagnostic stage bench */
 template <class KS, int VAR = 0>
 WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nb = m->nbody, nlevel = pl->nlevel;
   const int b = lane < nb ? lane : 0;
   const int depth = (lane < nb && lane > 0) ? pl->body_depth[b] : -1;
@@ -774,7 +774,7 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
    values, so one level sweep produces cvel, cdof_dot and cacc */
 template <class KS>
 WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nb = m->nbody, nlevel = pl->nlevel;
   const int b = lane < nb ? lane : 0;
   const int depth = (lane < nb && lane > 0) ? pl->body_depth[b] : -1;
@@ -847,7 +847,7 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
    (i = nb-1 .. 1, parent += child) as a readlane chain, written to LDS for qfrc_bias */
 template <class KS>
 WD void r_cfrc(KModel m, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nb = m->nbody;
   double (*cacc)[10] = s.u.body.b10;
   double (*cfrc)[6] = s.u.body.b6;
@@ -896,7 +896,7 @@ WD void r_cfrc(KModel m, KS& s) {
    bails (ovf): the full-capacity tier then reproduces the oracle's truncation rule. */
 template <class KS>
 WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nj = m->njnt, ncon = s.ncon;
   int lo = 0, hi = 0;
   if (lane < nj && m->jnt_limited[lane] &&
@@ -957,7 +957,7 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
    Same expressions as w_make_constraint's phases A and B. */
 template <class KS>
 WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
-  const int lane = threadIdx.x;
+  const int lane = w_lane();
   const int nv = NVOF(KS, m);
   const int ngrp = s.ngrp, nefc = s.nefc;
   /* ---- 1. per-group data (lane = group) ---- */
