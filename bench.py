@@ -236,7 +236,7 @@ def main():
             "data": "synthetic (uniform random actions in the ur3e-v2 action Box; stochastic 'high' mug resets)",
             "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
-                       "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (LDS working set, 4 envs/CU)"
+                       "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (20 KB lifetime-overlaid LDS working set, 256 VGPRs: 8 envs/CU, 2 per SIMD)"
                                             " + full-capacity fallback", -128: "full-capacity, 128 lanes per env",
                                             -64: "full-capacity, 64 lanes per env"}.get(
                            batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),

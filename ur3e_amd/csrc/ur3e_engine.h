@@ -698,7 +698,9 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
   double ic[3] = {ip[0] + isg * is[im] * ia[im][0], ip[1] + isg * is[im] * ia[im][1],
                   ip[2] + isg * is[im] * ia[im][2]};
   int u1 = (im + 1) % 3, u2 = (im + 2) % 3;
-  double poly[16][3], tmp[16][3];
+  /* a quad clipped by the 4 half-planes of a rectangle never exceeds 8 vertices (each clip adds
+     at most one), so 8-point buffers hold every intermediate polygon */
+  double poly[8][3], tmp[8][3];
   int np = 4;
   const double sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
   for (int k = 0; k < 4; k++) {
