@@ -6,7 +6,7 @@ sys.path.insert(0, REPO)
 LIB = os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_timing.so")
 if not os.path.exists(LIB):
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-                    "-shared", "-Wno-unused-result", "-DUR3E_STAGE_TIMING", "-o", LIB,
+                    "-shared", "-Wno-unused-result", "-DUR3E_STAGE_TIMING", "-DW_SMALL_MAXCON=9", "-o", LIB,
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip"),
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_vecnorm.hip")], check=True)
 os.environ["UR3E_LIB"] = LIB

@@ -161,7 +161,7 @@ struct KSX<MC, ME, NVC, TREE, true> {
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
   unsigned long long tlast;
 #ifdef UR3E_STAGE_TIMING
-  unsigned long long tacc[32];
+  unsigned int tacc[32]; /* 32-bit: keeps the timing build's layout within 20 KB (with MAXCON 9) */
   unsigned int tcnt[32];
 #endif
   union {
@@ -276,7 +276,7 @@ __device__ unsigned long long ur3e_stage_calls[32];
   do {                                                                  \
     __builtin_amdgcn_wave_barrier();                                    \
     if (w_lane() < 32 && s.tcnt[w_lane()]) {                      \
-      atomicAdd(&ur3e_stage_cycles[w_lane()], s.tacc[w_lane()]);  \
+      atomicAdd(&ur3e_stage_cycles[w_lane()], (unsigned long long)s.tacc[w_lane()]);  \
       atomicAdd(&ur3e_stage_calls[w_lane()], (unsigned long long)s.tcnt[w_lane()]); \
     }                                                                   \
   } while (0)
