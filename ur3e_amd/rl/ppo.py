@@ -1,0 +1,213 @@
+"""Device-resident PPO driving the batched env (BASELINE config C5).
+
+Replaces `stable_baselines3.PPO("MlpPolicy", VecNormalize(venv), ...)` as configured in
+gymnasium_src/scripts/regular_rl/rl/train_rl.py:60-73 with gymnasium_src/config/config_rl.yml
+(net_arch [256, 256], lr 3e-4, batch 256, n_epochs 30, gamma 0.99, gae_lambda 0.95, ent_coef 0.01;
+SB3 defaults for the rest: clip_range 0.2, vf_coef 0.5, max_grad_norm 0.5, Adam eps 1e-5,
+normalize_advantage, state-independent log_std initialised to 0, tanh MLPs with orthogonal init).
+SB3 itself is not installed in this image; the algorithm follows stable_baselines3==2.x
+(`PPO.train`, `OnPolicyAlgorithm.collect_rollouts`, `RolloutBuffer.compute_returns_and_advantage`).
+
+MI355X layout: the env, the on-device VecNormalize, the rollout buffer and the policy all live on
+one GPU and share torch's current stream, so a rollout step is env kernel -> normalisation kernel ->
+policy forward with no host round trip.  With several ranks (one process per GPU) each rank steps its
+own env shard and keeps a policy replica; gradients are flattened into ONE buffer and all-reduced
+(averaged) per minibatch, a single RCCL call over xGMI instead of one per parameter tensor.
+
+The env object only needs `num_envs`, `action_space` (low/high), `reset_torch()` and
+`step_torch(actions) -> (obs f32, reward, terminated, truncated, terminal_obs f32)`: the GPU
+`VecNormalize` provides it, and tests use a CPU stand-in with the same interface.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import torch
+import torch.nn as nn
+
+
+def _mlp(sizes, gain):
+    layers = []
+    for i in range(len(sizes) - 1):
+        lin = nn.Linear(sizes[i], sizes[i + 1])
+        nn.init.orthogonal_(lin.weight, gain=gain)
+        nn.init.zeros_(lin.bias)
+        layers += [lin, nn.Tanh()]
+    return nn.Sequential(*layers)
+
+
+class ActorCritic(nn.Module):
+    """SB3 ActorCriticPolicy for a Box action space with net_arch=[256, 256]: separate pi / vf MLPs
+    over the flattened observation, Gaussian head with a state-independent log_std."""
+
+    def __init__(self, obs_dim: int, act_dim: int, net_arch=(256, 256), log_std_init: float = 0.0):
+        super().__init__()
+        self.pi_net = _mlp([obs_dim, *net_arch], gain=math.sqrt(2))
+        self.vf_net = _mlp([obs_dim, *net_arch], gain=math.sqrt(2))
+        self.action_net = nn.Linear(net_arch[-1], act_dim)
+        self.value_net = nn.Linear(net_arch[-1], 1)
+        nn.init.orthogonal_(self.action_net.weight, gain=0.01)
+        nn.init.zeros_(self.action_net.bias)
+        nn.init.orthogonal_(self.value_net.weight, gain=1.0)
+        nn.init.zeros_(self.value_net.bias)
+        self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+
+    def dist(self, obs):
+        mean = self.action_net(self.pi_net(obs))
+        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean))
+
+    def value(self, obs):
+        return self.value_net(self.vf_net(obs)).squeeze(-1)
+
+    def evaluate(self, obs, actions):
+        d = self.dist(obs)
+        return self.value(obs), d.log_prob(actions).sum(-1), d.entropy().sum(-1)
+
+
+def compute_gae(rewards, values, episode_starts, last_values, dones, gamma, lam):
+    """RolloutBuffer.compute_returns_and_advantage: rewards/values/episode_starts [T, N];
+    `dones` are the done flags after the last step. Returns (advantages, returns)."""
+    T = rewards.shape[0]
+    adv = torch.zeros_like(rewards)
+    last = torch.zeros_like(last_values)
+    for t in reversed(range(T)):
+        if t == T - 1:
+            nonterm = 1.0 - dones.to(rewards.dtype)
+            nv = last_values
+        else:
+            nonterm = 1.0 - episode_starts[t + 1]
+            nv = values[t + 1]
+        delta = rewards[t] + gamma * nv * nonterm - values[t]
+        last = delta + gamma * lam * nonterm * last
+        adv[t] = last
+    return adv, adv + values
+
+
+class PPO:
+    def __init__(self, env, n_steps: int = 16, batch_size: int = 256, n_epochs: int = 30, learning_rate: float = 3e-4,
+                 gamma: float = 0.99, gae_lambda: float = 0.95, clip_range: float = 0.2, ent_coef: float = 0.01,
+                 vf_coef: float = 0.5, max_grad_norm: float = 0.5, net_arch=(256, 256), device=None, seed: int = 0,
+                 group=None):
+        self.env = env
+        self.n_envs = env.num_envs
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        low = torch.as_tensor(env.action_space.low, dtype=torch.float32, device=self.device)
+        high = torch.as_tensor(env.action_space.high, dtype=torch.float32, device=self.device)
+        self.low, self.high = low, high
+        self.obs_dim = env.observation_space.shape[0]
+        self.act_dim = low.numel()
+        self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
+        self.gamma, self.lam, self.clip, self.ent_coef, self.vf_coef = gamma, gae_lambda, clip_range, ent_coef, vf_coef
+        self.max_grad_norm = max_grad_norm
+        self.group = group
+        torch.manual_seed(seed)
+        self.policy = ActorCritic(self.obs_dim, self.act_dim, net_arch).to(self.device)
+        if group is not None:  # identical replicas: broadcast rank 0's initial weights
+            import torch.distributed as dist
+            for p in self.policy.parameters():
+                dist.broadcast(p.data, src=0, group=group)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        T, N, f = n_steps, self.n_envs, dict(dtype=torch.float32, device=self.device)
+        self.buf_obs = torch.zeros((T, N, self.obs_dim), **f)
+        self.buf_act = torch.zeros((T, N, self.act_dim), **f)
+        self.buf_rew = torch.zeros((T, N), **f)
+        self.buf_start = torch.zeros((T, N), **f)
+        self.buf_val = torch.zeros((T, N), **f)
+        self.buf_logp = torch.zeros((T, N), **f)
+        self._last_obs = None
+        self._last_start = torch.ones(N, **f)
+        self.num_timesteps = 0
+        self.stats = {}
+
+    # -- rollout ---------------------------------------------------------------
+    @torch.no_grad()
+    def collect_rollouts(self):
+        if self._last_obs is None:
+            self._last_obs = self.env.reset_torch().to(torch.float32)
+        done = None
+        for t in range(self.n_steps):
+            obs = self._last_obs
+            d = self.policy.dist(obs)
+            noise = torch.randn(d.mean.shape, generator=self.gen, device=self.device, dtype=d.mean.dtype)
+            act = d.mean + d.stddev * noise
+            val = self.policy.value(obs)
+            logp = d.log_prob(act).sum(-1)
+            clipped = torch.maximum(torch.minimum(act, self.high), self.low)
+            nobs, rew, term, trunc, tobs = self.env.step_torch(clipped.to(torch.float64))
+            rew = rew.to(torch.float32)
+            term, trunc = term.bool(), trunc.bool()
+            done = term | trunc
+            # SB3 timeout bootstrap: truncated-not-terminated envs get gamma * V(terminal obs); evaluated
+            # for every env and masked, so the rollout never waits on the host for an any()
+            boot = (trunc & ~term).to(torch.float32)
+            rew = rew + self.gamma * torch.where(boot > 0, self.policy.value(tobs.to(torch.float32)),
+                                                 torch.zeros_like(rew))
+            self.buf_obs[t], self.buf_act[t], self.buf_rew[t] = obs, act, rew
+            self.buf_start[t], self.buf_val[t], self.buf_logp[t] = self._last_start, val, logp
+            self._last_obs = nobs.to(torch.float32).clone()  # the env reuses its output buffer
+            self._last_start = done.to(torch.float32)
+        last_val = self.policy.value(self._last_obs)
+        self.adv, self.ret = compute_gae(self.buf_rew, self.buf_val, self.buf_start, last_val, done, self.gamma,
+                                         self.lam)
+        self.num_timesteps += self.n_steps * self.n_envs
+
+    # -- update ----------------------------------------------------------------
+    def _allreduce_grads(self):
+        import torch.distributed as dist
+        params = [p for p in self.policy.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        dist.all_reduce(flat, group=self.group)
+        flat /= dist.get_world_size(self.group)
+        off = 0
+        for p in params:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
+    def train(self):
+        T, N = self.n_steps, self.n_envs
+        obs = self.buf_obs.reshape(T * N, -1)
+        act = self.buf_act.reshape(T * N, -1)
+        old_logp, old_val = self.buf_logp.reshape(-1), self.buf_val.reshape(-1)
+        adv_all, ret_all = self.adv.reshape(-1), self.ret.reshape(-1)
+        total = T * N
+        last = {}
+        for _ in range(self.n_epochs):
+            perm = torch.randperm(total, generator=self.gen, device=self.device)
+            for s in range(0, total, self.batch_size):
+                idx = perm[s:s + self.batch_size]
+                v, logp, ent = self.policy.evaluate(obs[idx], act[idx])
+                adv = adv_all[idx]
+                if adv.numel() > 1:
+                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                ratio = torch.exp(logp - old_logp[idx])
+                pg = -torch.min(adv * ratio, adv * ratio.clamp(1 - self.clip, 1 + self.clip)).mean()
+                vf = torch.nn.functional.mse_loss(ret_all[idx], v)
+                ent_loss = -ent.mean()
+                loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+                self.opt.zero_grad(set_to_none=False)
+                loss.backward()
+                if self.group is not None:
+                    self._allreduce_grads()
+                nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                self.opt.step()
+                last = {"policy_gradient_loss": pg.detach(), "value_loss": vf.detach(), "entropy_loss": ent_loss.detach()}
+        self.stats = {k: float(v) for k, v in last.items()}
+
+    def learn(self, iterations: int = 1):
+        """Returns per-iteration wall times {rollout_s, train_s}."""
+        times = []
+        for _ in range(iterations):
+            t0 = time.perf_counter()
+            self.collect_rollouts()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            t1 = time.perf_counter()
+            self.train()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            times.append({"rollout_s": t1 - t0, "train_s": time.perf_counter() - t1})
+        return times
