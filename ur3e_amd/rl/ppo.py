@@ -55,7 +55,8 @@ class ActorCritic(nn.Module):
 
     def dist(self, obs):
         mean = self.action_net(self.pi_net(obs))
-        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean))
+        # validate_args=False: the argument checks synchronise with the host every rollout step
+        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean), validate_args=False)
 
     def value(self, obs):
         return self.value_net(self.vf_net(obs)).squeeze(-1)
@@ -117,41 +118,48 @@ class PPO:
         self.buf_start = torch.zeros((T, N), **f)
         self.buf_val = torch.zeros((T, N), **f)
         self.buf_logp = torch.zeros((T, N), **f)
-        self._last_obs = None
-        self._last_start = torch.ones(N, **f)
+        self._noise = torch.zeros((T, N, self.act_dim), **f)
+        self._obs = None
+        self._start = torch.ones(N, **f)
         self.num_timesteps = 0
         self.stats = {}
 
     # -- rollout ---------------------------------------------------------------
+    def _rollout_step(self, t: int):
+        """One env step at rollout index t (persistent tensors; no host synchronisation)."""
+        obs = self._obs
+        d = self.policy.dist(obs)
+        act = d.mean + d.stddev * self._noise[t]
+        val = self.policy.value(obs)
+        logp = d.log_prob(act).sum(-1)
+        clipped = torch.maximum(torch.minimum(act, self.high), self.low)
+        nobs, rew, term, trunc, tobs = self.env.step_torch(clipped.to(torch.float64))
+        rew = rew.to(torch.float32)
+        term, trunc = term.bool(), trunc.bool()
+        # SB3 timeout bootstrap: truncated-not-terminated envs get gamma * V(terminal obs); evaluated
+        # for every env and masked, so the rollout never waits on the host for an any()
+        boot = trunc & ~term
+        rew = rew + self.gamma * torch.where(boot, self.policy.value(tobs.to(torch.float32)), torch.zeros_like(rew))
+        self.buf_obs[t].copy_(obs)
+        self.buf_act[t].copy_(act)
+        self.buf_rew[t].copy_(rew)
+        self.buf_start[t].copy_(self._start)
+        self.buf_val[t].copy_(val)
+        self.buf_logp[t].copy_(logp)
+        self._obs.copy_(nobs)  # the env reuses its output buffers: copy, never alias
+        self._start.copy_((term | trunc).to(torch.float32))
+
     @torch.no_grad()
     def collect_rollouts(self):
-        if self._last_obs is None:
-            self._last_obs = self.env.reset_torch().to(torch.float32)
-        done = None
+        if self._obs is None:
+            self._obs = self.env.reset_torch().to(torch.float32).clone()
+        # all sampling noise of the rollout in one draw
+        self._noise.normal_(generator=self.gen)
         for t in range(self.n_steps):
-            obs = self._last_obs
-            d = self.policy.dist(obs)
-            noise = torch.randn(d.mean.shape, generator=self.gen, device=self.device, dtype=d.mean.dtype)
-            act = d.mean + d.stddev * noise
-            val = self.policy.value(obs)
-            logp = d.log_prob(act).sum(-1)
-            clipped = torch.maximum(torch.minimum(act, self.high), self.low)
-            nobs, rew, term, trunc, tobs = self.env.step_torch(clipped.to(torch.float64))
-            rew = rew.to(torch.float32)
-            term, trunc = term.bool(), trunc.bool()
-            done = term | trunc
-            # SB3 timeout bootstrap: truncated-not-terminated envs get gamma * V(terminal obs); evaluated
-            # for every env and masked, so the rollout never waits on the host for an any()
-            boot = (trunc & ~term).to(torch.float32)
-            rew = rew + self.gamma * torch.where(boot > 0, self.policy.value(tobs.to(torch.float32)),
-                                                 torch.zeros_like(rew))
-            self.buf_obs[t], self.buf_act[t], self.buf_rew[t] = obs, act, rew
-            self.buf_start[t], self.buf_val[t], self.buf_logp[t] = self._last_start, val, logp
-            self._last_obs = nobs.to(torch.float32).clone()  # the env reuses its output buffer
-            self._last_start = done.to(torch.float32)
-        last_val = self.policy.value(self._last_obs)
-        self.adv, self.ret = compute_gae(self.buf_rew, self.buf_val, self.buf_start, last_val, done, self.gamma,
-                                         self.lam)
+            self._rollout_step(t)
+        last_val = self.policy.value(self._obs)
+        self.adv, self.ret = compute_gae(self.buf_rew, self.buf_val, self.buf_start, last_val, self._start > 0,
+                                         self.gamma, self.lam)
         self.num_timesteps += self.n_steps * self.n_envs
 
     # -- update ----------------------------------------------------------------
