@@ -155,6 +155,21 @@ WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV]) {
   return v;
 }
 
+/* Ordered sums and vector broadcasts inside Newton go through a 64-double LDS slot per operand
+   (the packed-Hessian bytes, unused outside r_direction): each lane stores its value, then every
+   lane reads the slot in order with broadcast ds_reads, which issue back to back, instead of a
+   chain of v_readlane pairs.  Same operands, same order, so the sums are unchanged. */
+#define R_SLOT(s, k) ((s).Hl + 64 * (k))
+WD void r_stage(double* slot, double v) {
+  slot[w_lane()] = v;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+WD void r_slot_done() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 /* uniform copy of a dof vector held one element per lane */
 WD void r_bcast(double v, int nv, double out[K_NV]) {
 #pragma unroll
@@ -163,12 +178,14 @@ WD void r_bcast(double v, int nv, double out[K_NV]) {
 
 /* w_eval_state: Ma (lane k), jar/force/cost terms (lane r), gauss and cost (uniform) */
 template <class KS>
-WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
+WD void r_eval_state(KModel m, KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
                      double& cost) {
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double qv[K_NV];
-  r_bcast(qacc, nv, qv);
+  r_stage(R_SLOT(s, 0), lane < nv ? qacc : 0.0);
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) qv[k] = R_SLOT(s, 0)[k];
   {
     double v = 0;
     const int row = lane < nv ? lane : 0;
@@ -181,13 +198,19 @@ WD void r_eval_state(KModel m, const KS& s, RRow& w, double qacc, double qs, dou
   r_constraint_update(w);
   double term = (Ma - qs) * (qacc - qas);
   double a0 = 0, a1 = 0;
-#pragma unroll
-  for (int i = 0; i < K_NV; i++)
-    if (i < nv) a0 += rl(term, i);
   /* skipped rows contribute -0.0: x + (-0.0) == x exactly for every x (incl. -0, inf, NaN), so
      the ordered sum needs neither a branch nor a select per row */
   const double Fm0 = w.flag ? w.F : -0.0;
-  for (int i = 0; i < nefc; i++) a1 += rl(Fm0, i);
+  double* st = R_SLOT(s, 1);
+  double* sf = R_SLOT(s, 2);
+  st[lane] = term;
+  r_stage(sf, Fm0);
+#pragma unroll
+  for (int i = 0; i < K_NV; i++)
+    if (i < nv) a0 += st[i];
+#pragma unroll 4
+  for (int i = 0; i < nefc; i++) a1 += sf[i];
+  r_slot_done();
   gauss = 0.5 * a0;
   cost = gauss + a1;
 }
@@ -379,9 +402,9 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 }
 
 /* line-search 1-D evaluation at a (w_ls_eval): per-row terms on the row lanes, ordered sums */
-template <int ME>
-WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF, double& lsdF,
-                  double& lsd2F) {
+template <class KS>
+WD void r_ls_eval(KS& s, const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF,
+                  double& lsdF, double& lsd2F) {
   const int lane = w_lane();
   const double D = w.D, R = w.R;
   double x = w.jar + a * w.Jv;
@@ -437,11 +460,17 @@ WD void r_ls_eval(const RRow& w, int nefc, double a, double gauss, double g1, do
   double ad2F = g2;
   /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
   const double Fm = flag ? F : -0.0, dFm = flag ? dF : -0.0, d2Fm = flag == 1 ? d2F : -0.0;
+  double *b0 = R_SLOT(s, 0), *b1 = R_SLOT(s, 1), *b2 = R_SLOT(s, 2);
+  b0[lane] = Fm;
+  b1[lane] = dFm;
+  r_stage(b2, d2Fm);
+#pragma unroll 4
   for (int i = 0; i < nefc; i++) {
-    aF += rl(Fm, i);
-    adF += rl(dFm, i);
-    ad2F += rl(d2Fm, i);
+    aF += b0[i];
+    adF += b1[i];
+    ad2F += b2[i];
   }
+  r_slot_done();
   lsF = aF; lsdF = adF; lsd2F = ad2F;
 }
 
@@ -452,7 +481,10 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double sv[K_NV];
-  r_bcast(search, nv, sv);
+  r_stage(R_SLOT(s, 0), lane < nv ? search : 0.0);
+#pragma unroll
+  for (int k = 0; k < K_NV; k++) sv[k] = R_SLOT(s, 0)[k];
+  r_slot_done();
   double sn = 0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++)
@@ -471,16 +503,19 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
   double g1 = 0, g2 = 0;
+  R_SLOT(s, 1)[lane] = t1;
+  r_stage(R_SLOT(s, 2), t2);
 #pragma unroll
   for (int k = 0; k < K_NV; k++) {
     if (k < nv) {
-      g1 += rl(t1, k);
-      g2 += rl(t2, k);
+      g1 += R_SLOT(s, 1)[k];
+      g2 += R_SLOT(s, 2)[k];
     }
   }
+  r_slot_done();
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
-  r_ls_eval<KS::MAXEFC>(w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
+  r_ls_eval(s, w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
   if (d0 >= 0) return 0;
   double lo = 0.0, dlo = d0, hlo = h0;
   double hi = -1.0, dhi = 0, hhi = 0;
@@ -489,7 +524,7 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   WT(19);
   for (int it = 0; it < m->ls_iterations; it++) {
     double f, df, d2f;
-    r_ls_eval<KS::MAXEFC>(w, nefc, a, gauss, g1, g2, f, df, d2f);
+    r_ls_eval(s, w, nefc, a, gauss, g1, g2, f, df, d2f);
     WT(20);
     if (f < bestF) { bestF = f; bestA = a; }
     if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
