@@ -217,15 +217,18 @@ WD void r_eval_state(KModel m, KS& s, RRow& w, double qacc, double qs, double qa
 
 /* w_compute_grad: lane k: qfrc_constraint[k] = sum_i J[i][k] force[i] (row order), grad */
 template <class KS>
-WD void r_compute_grad(KModel m, const KS& s, const RRow& w, double Ma, double qs, double& qfrc_c, double& grad) {
+WD void r_compute_grad(KModel m, KS& s, const RRow& w, double Ma, double qs, double& qfrc_c, double& grad) {
   const int lane = w_lane();
   const int nefc = s.nefc;
   const int col = lane < K_NV ? lane : 0;
   double f = 0;
-  /* partially unrolled: a fully unrolled MAXEFC-row loop hoists every J load and force
-     broadcast at once (88 live VGPRs) */
+  /* row forces broadcast from an LDS slot; partially unrolled: a fully unrolled MAXEFC-row loop
+     hoists every J load at once */
+  double* fs = R_SLOT(s, 0);
+  r_stage(fs, w.force);
 #pragma unroll 4
-  for (int i = 0; i < nefc; i++) f = f + s.efc_J[i][col] * rl(w.force, i);
+  for (int i = 0; i < nefc; i++) f = f + s.efc_J[i][col] * fs[i];
+  r_slot_done();
   qfrc_c = f;
   grad = Ma - qs - f;
 }
@@ -588,9 +591,14 @@ WD void r_solve_newton(KModel m, KS& s) {
     r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
     WT(14);
     double gn = 0;
+    r_stage(R_SLOT(s, 0), grad);
 #pragma unroll
     for (int i = 0; i < K_NV; i++)
-      if (i < nv) gn += rl(grad, i) * rl(grad, i);
+      if (i < nv) {
+        const double gi = R_SLOT(s, 0)[i];
+        gn += gi * gi;
+      }
+    r_slot_done();
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
