@@ -295,17 +295,25 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
   /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
      compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
      trips per element) */
+  /* only rows that add to H are visited, in row order (the others add nothing in the oracle):
+     quadratic rows and the first row of each cone-state contact */
+  const bool adds = lane < nefc && (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC &&
+                                                               w.jj == 0));
+  unsigned long long act = __ballot(adds);
+  const int ifirst = act ? (int)__builtin_ctzll(act) : 0;
   double njk[NQ], njc[NQ];
 #pragma unroll
-  for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[0][ek[q]]; njc[q] = s.efc_J[0][ec[q]]; }
-  for (int i = 0; i < nefc; i++) {
+  for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[ifirst][ek[q]]; njc[q] = s.efc_J[ifirst][ec[q]]; }
+  while (act) {
+    const int i = (int)__builtin_ctzll(act);
+    act &= act - 1;
     double jk[NQ], jc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
       jk[q] = njk[q]; jc[q] = njc[q];
       asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
     }
-    const int inext = i + 1 < KS::MAXEFC ? i + 1 : i;
+    const int inext = act ? (int)__builtin_ctzll(act) : i;
 #pragma unroll
     for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[inext][ek[q]]; njc[q] = s.efc_J[inext][ec[q]]; }
     const int st = rli(w.st, i);
