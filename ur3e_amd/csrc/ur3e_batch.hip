@@ -1224,6 +1224,20 @@ static int check_model(const ur3e_model_t* m) {
 
 static void build_plan(const ur3e_model_t* m, KPlan* pl) {
   memset(pl, 0, sizeof(*pl));
+  for (int a = 0; a < m->nu; a++) {
+    const double g = m->act_gear[a];
+    for (int v = 0; v < m->nv; v++) {
+      double mom = 0;
+      if (m->act_trntype[a] == UR3E_TRN_JOINT) {
+        mom = (v == m->jnt_dofadr[m->act_trnid[a]]) ? g : 0.0;
+      } else {
+        const int t = m->act_trnid[a];
+        for (int k = 0; k < m->ten_num[t]; k++)
+          if (m->ten_dof[t][k] == v) mom = m->ten_coef[t][k] * g; /* same product as the oracle */
+      }
+      pl->act_moment[a][v] = mom;
+    }
+  }
   int nl = 0;
   for (int i = 1; i < m->nbody; i++) {
     pl->body_depth[i] = pl->body_depth[m->body_parentid[i]] + 1;

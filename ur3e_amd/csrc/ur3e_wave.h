@@ -44,6 +44,9 @@ struct KPlan {
   /* row groups that exist every step (equality, then frictionloss), in oracle order */
   int nfixgrp, nfixrow;
   int fix_type[UR3E_MAXEQ + K_NV], fix_id[UR3E_MAXEQ + K_NV], fix_row[UR3E_MAXEQ + K_NV];
+  /* actuator moment arm per dof (mj_transmission: gear for a joint transmission, coef * gear for
+     each dof of a fixed tendon, 0 elsewhere); model constants, so computed once on the host */
+  double act_moment[K_NU][K_NV];
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -1067,20 +1070,8 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
     s.qfrc_passive[v] = pf;
   }
   for (int a = tid; a < m->nu; a += NT) {
-    double g = m->act_gear[a];
     double vel = 0;
-    if (m->act_trntype[a] == UR3E_TRN_JOINT) {
-      int dof = m->jnt_dofadr[m->act_trnid[a]];
-      for (int v = 0; v < nv; v++) vel += (v == dof ? g : 0.0) * s.qvel[v];
-    } else {
-      int t = m->act_trnid[a];
-      for (int v = 0; v < nv; v++) {
-        double mom = 0;
-        for (int k = 0; k < m->ten_num[t]; k++)
-          if (m->ten_dof[t][k] == v) mom = m->ten_coef[t][k] * g;
-        vel += mom * s.qvel[v];
-      }
-    }
+    for (int v = 0; v < nv; v++) vel += pl->act_moment[a][v] * s.qvel[v];
     double ctrl = s.ctrl[a];
     if (m->act_ctrllimited[a]) {
       if (ctrl < m->act_ctrlrange[a][0]) ctrl = m->act_ctrlrange[a][0];
@@ -1099,18 +1090,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if (tid < nv) {
     int v = tid;
     double sa = 0;
-    for (int a = 0; a < m->nu; a++) {
-      double mom;
-      if (m->act_trntype[a] == UR3E_TRN_JOINT) {
-        mom = (v == m->jnt_dofadr[m->act_trnid[a]]) ? m->act_gear[a] : 0.0;
-      } else {
-        int t = m->act_trnid[a];
-        mom = 0;
-        for (int k = 0; k < m->ten_num[t]; k++)
-          if (m->ten_dof[t][k] == v) mom = m->ten_coef[t][k] * m->act_gear[a];
-      }
-      sa += mom * s.act_force[a];
-    }
+    for (int a = 0; a < m->nu; a++) sa += pl->act_moment[a][v] * s.act_force[a];
     s.qfrc_smooth[v] = s.qfrc_passive[v] - s.qfrc_bias[v] + sa;
   }
   SYNC();
