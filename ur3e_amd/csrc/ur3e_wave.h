@@ -386,25 +386,48 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
     } else {
       k_local2global(xipos, ximat, s.xpos[i], s.xquat[i], s.xmat[i], m->body_ipos[i], m->body_iquat[i]);
     }
-    s.subtree_com[i][0] = xipos[0] * m->body_mass[i];
-    s.subtree_com[i][1] = xipos[1] * m->body_mass[i];
-    s.subtree_com[i][2] = xipos[2] * m->body_mass[i];
   }
-  SYNC();
-  if (tid < 3) {
-    for (int i = nb - 1; i > 0; i--) s.subtree_com[m->body_parentid[i]][tid] += s.subtree_com[i][tid];
-  }
-  SYNC();
-  if (tid < nb) {
-    int i = tid;
-    if (m->body_subtreemass[i] < K_MINVAL) {
-      s.subtree_com[i][0] = xipos[0]; s.subtree_com[i][1] = xipos[1]; s.subtree_com[i][2] = xipos[2];
-    } else {
-      double sc = 1.0 / m->body_subtreemass[i];
-      s.subtree_com[i][0] *= sc; s.subtree_com[i][1] *= sc; s.subtree_com[i][2] *= sc;
+  if constexpr (NT == 64) {
+    /* mass-weighted positions summed up the tree in registers (r_subtree_sum) */
+    double sm[3] = {0, 0, 0};
+    if (tid < nb) {
+      const double mass = m->body_mass[tid];
+      sm[0] = xipos[0] * mass; sm[1] = xipos[1] * mass; sm[2] = xipos[2] * mass;
     }
+    r_subtree_sum<3, false>(m, sm);
+    if (tid < nb) {
+      const int i = tid;
+      if (m->body_subtreemass[i] < K_MINVAL) {
+        s.subtree_com[i][0] = xipos[0]; s.subtree_com[i][1] = xipos[1]; s.subtree_com[i][2] = xipos[2];
+      } else {
+        double sc = 1.0 / m->body_subtreemass[i];
+        s.subtree_com[i][0] = sm[0] * sc; s.subtree_com[i][1] = sm[1] * sc; s.subtree_com[i][2] = sm[2] * sc;
+      }
+    }
+    SYNC();
+  } else {
+    if (tid < nb) {
+      int i = tid;
+      s.subtree_com[i][0] = xipos[0] * m->body_mass[i];
+      s.subtree_com[i][1] = xipos[1] * m->body_mass[i];
+      s.subtree_com[i][2] = xipos[2] * m->body_mass[i];
+    }
+    SYNC();
+    if (tid < 3) {
+      for (int i = nb - 1; i > 0; i--) s.subtree_com[m->body_parentid[i]][tid] += s.subtree_com[i][tid];
+    }
+    SYNC();
+    if (tid < nb) {
+      int i = tid;
+      if (m->body_subtreemass[i] < K_MINVAL) {
+        s.subtree_com[i][0] = xipos[0]; s.subtree_com[i][1] = xipos[1]; s.subtree_com[i][2] = xipos[2];
+      } else {
+        double sc = 1.0 / m->body_subtreemass[i];
+        s.subtree_com[i][0] *= sc; s.subtree_com[i][1] *= sc; s.subtree_com[i][2] *= sc;
+      }
+    }
+    SYNC();
   }
-  SYNC();
   for (int j = tid; j < m->njnt; j += NT) {
     int b = m->jnt_bodyid[j];
     int da = m->jnt_dofadr[j];
@@ -494,23 +517,34 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
 /* CRB mass matrix + tree LDL'                                         */
 /* ================================================================== */
 template <int NT, class KS>
-WD void w_crb(KModel m, KS& s) {
+WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nb = m->nbody, nv = NVOF(KS, m);
-  for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
+  if constexpr (NT == 64) {
+    /* composite inertias summed up the tree in registers (lane = body) */
+    double crb[10];
+    for (int k = 0; k < 10; k++) crb[k] = tid < nb ? s.cinert[tid][k] : 0.0;
+    r_subtree_sum<10, true>(m, crb);
+    if (tid < nb)
+      for (int k = 0; k < 10; k++) s.u.body.b10[tid][k] = crb[k];
+  } else {
+    for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
+  }
   if constexpr (KS::OVERLAY) {
     for (int e = tid; e < nv * (nv + 1) / 2; e += NT) s.qMp[e] = 0;
   } else {
     for (int e = tid; e < nv * nv; e += NT) s.qM[e / nv][e % nv] = 0;
   }
   SYNC();
-  if (tid < 10) {
-    for (int i = nb - 1; i > 0; i--) {
-      int p = m->body_parentid[i];
-      if (p > 0) s.u.body.b10[p][tid] += s.u.body.b10[i][tid];
+  if constexpr (NT != 64) {
+    if (tid < 10) {
+      for (int i = nb - 1; i > 0; i--) {
+        int p = m->body_parentid[i];
+        if (p > 0) s.u.body.b10[p][tid] += s.u.body.b10[i][tid];
+      }
     }
+    SYNC();
   }
-  SYNC();
   if (tid < nv) {
     int i = tid;
     double buf[6];
@@ -519,7 +553,10 @@ WD void w_crb(KModel m, KS& s) {
     mii += k_dot6(s.cdof[i], buf);
     if constexpr (KS::OVERLAY) s.qMp[KTRI(i, i)] = mii;
     else s.qM[i][i] = mii;
-    for (int j = m->dof_parentid[i]; j >= 0; j = m->dof_parentid[j]) {
+    /* ancestors nearest first, from the plan (independent loads instead of a parent-pointer chase) */
+    const int na = pl->dof_nanc[i];
+    for (int k = 0; k < na; k++) {
+      const int j = pl->dof_anc[i][k];
       double v = 0.0;
       v += k_dot6(s.cdof[j], buf);
       if constexpr (KS::OVERLAY) {
@@ -1569,7 +1606,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   WT(0);
   w_com_pos<NT>(m, pl, s);
   WT(1);
-  w_crb<NT>(m, s);
+  w_crb<NT>(m, pl, s);
   if constexpr (!REG) {
     for (int e = tid; e < nv * nv; e += NT) s.H[e / nv][e % nv] = s.qM[e / nv][e % nv];
     SYNC();

@@ -707,6 +707,33 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   return x;
 }
 
+/* subtree accumulation f[parent(i)] += f[i] for i = nbody-1 .. 1 (the oracle's order), lane = body,
+   as a readlane chain in registers instead of read-modify-write round trips through LDS;
+   SKIP_WORLD leaves body 0 out (crb) */
+template <int C, bool SKIP_WORLD>
+WD void r_subtree_sum(KModel m, double (&f)[C]) {
+  const int lane = w_lane();
+  const int nb = m->nbody;
+  int par[K_NB];
+#pragma unroll
+  for (int i = 0; i < K_NB; i++) par[i] = i < nb ? m->body_parentid[i] : 0;
+#pragma unroll
+  for (int i = K_NB - 1; i > 0; i--) {
+    if (i < nb) {
+      const int p = par[i];
+      if (!SKIP_WORLD || p > 0) {
+        double v[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) v[c] = rl(f[c], i);
+        if (lane == p) {
+#pragma unroll
+          for (int c = 0; c < C; c++) f[c] += v[c];
+        }
+      }
+    }
+  }
+}
+
 /* ================================================================== */
 /* body-tree passes for the compact tier (lane = body, nbody <= 64)    */
 /* ================================================================== */
