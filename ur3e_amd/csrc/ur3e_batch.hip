@@ -1224,6 +1224,11 @@ static int check_model(const ur3e_model_t* m) {
 
 static void build_plan(const ur3e_model_t* m, KPlan* pl) {
   memset(pl, 0, sizeof(*pl));
+  for (int t = 0; t < m->ntendon; t++)
+    for (int k = 0; k < m->ten_num[t]; k++) {
+      const int dof = m->ten_dof[t][k], j = m->dof_jntid[dof];
+      pl->ten_qadr[t][k] = m->jnt_qposadr[j] + (dof - m->jnt_dofadr[j]);
+    }
   for (int a = 0; a < m->nu; a++) {
     const double g = m->act_gear[a];
     for (int v = 0; v < m->nv; v++) {

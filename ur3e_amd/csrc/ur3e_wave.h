@@ -47,6 +47,7 @@ struct KPlan {
   /* actuator moment arm per dof (mj_transmission: gear for a joint transmission, coef * gear for
      each dof of a fixed tendon, 0 elsewhere); model constants, so computed once on the host */
   double act_moment[K_NU][K_NV];
+  int ten_qadr[UR3E_MAXTEN][UR3E_MAXTENWRAP]; /* qpos address of each fixed-tendon dof */
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -506,7 +507,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
     } else {
       int t = m->act_trnid[a];
       double len = 0;
-      for (int k = 0; k < m->ten_num[t]; k++) len += m->ten_coef[t][k] * s.qpos[k_dof_qposadr(m, m->ten_dof[t][k])];
+      for (int k = 0; k < m->ten_num[t]; k++) len += m->ten_coef[t][k] * s.qpos[pl->ten_qadr[t][k]];
       s.actuator_length[a] = len * g;
     }
   }
