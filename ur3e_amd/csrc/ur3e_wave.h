@@ -710,15 +710,16 @@ WD void r_collision(KModel m, KS& s) {
   int total = 0;
   for (int base = 0; base < nsurv; base += 64) {
     const int slot = base + lane;
-    /* every lane runs the narrowphase (idle lanes on survivor 0, result dropped) and the box-box
-       routine is inlined here: an out-of-line call from this divergent, register-saturated region
-       (256 VGPR + AGPR spill slots + ~760 SGPRs spilled to VGPR lanes) was miscompiled -- state
-       read after the forward pass came back corrupted -- while the inlined form is bit-exact */
+    /* the box-box routine is inlined here: an out-of-line call from this divergent region was
+       miscompiled in an earlier, register-saturated build (state read after the forward pass came
+       back corrupted), while the inlined form is bit-exact */
     const bool act = slot < nsurv;
     const int p = s.cand_off[act ? slot : 0];
     KRaw raw[8];
-    int cnt = w_narrow_core<KS, true>(m, s, p, raw);
-    cnt = act ? cnt : 0;
+    /* lanes without a survivor stay masked off, so their private-segment (scratch) stores of
+       the clip polygons and raw contacts never reach memory */
+    int cnt = 0;
+    if (act) cnt = w_narrow_core<KS, true>(m, s, p, raw);
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
