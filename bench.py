@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
     ap.add_argument("--cpu-sample-steps", type=int, default=1000)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather-self", action="store_true",
+                    help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
     args = ap.parse_args()
 
     import torch
@@ -118,9 +120,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.gather_self
+    if use_dist:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        # RCCL prints a version banner on stdout when the communicator comes up; keep stdout for
+        # the one JSON line by pointing fd 1 at stderr until the first collective has run
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
+            torch.cuda.synchronize()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -134,10 +154,13 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
 
-    gather = world > 1 and not args.no_gather
+    gather = use_dist and not args.no_gather
     if gather:
-        payload = torch.empty((n, 26), dtype=torch.float64, device=dev)
-        glist = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+        # double-buffered payload: step t's gather runs on its own stream while step t+1 computes
+        comm = torch.cuda.Stream(device=dev)
+        payloads = [torch.empty((n, 26), dtype=torch.float64, device=dev) for _ in range(2)]
+        glists = [[torch.empty_like(payloads[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+        nstep = [0]
 
     step_events = []
 
@@ -152,10 +175,17 @@ def main():
             e1.record()
             step_events.append((e0, e1))
         if gather:
+            k = nstep[0] & 1
+            nstep[0] += 1
+            payload = payloads[k]
+            # the gather that last read this buffer (two steps ago) must be done before it is refilled
+            torch.cuda.current_stream().wait_stream(comm)
             payload[:, :24] = obs
             payload[:, 24] = rew
             payload[:, 25] = (term | trunc).to(torch.float64)
-            dist.gather(payload, glist, dst=0)
+            comm.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(comm):
+                dist.gather(payload, glists[k], dst=0)
 
     for _ in range(args.warmup):
         one_step()
@@ -255,7 +285,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     batch.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
