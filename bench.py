@@ -78,6 +78,56 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0):
     return base, parity
 
 
+def other_configs(n_envs=4096, steps=50, warmup=5):
+    """Throughput of the BASELINE configs other than the headline one, on one GPU (rank 0, N=1):
+    C2 -- ur3e_2f85, random joint targets through move_j's PD (one mj_step per control step);
+    C3 -- main.xml move_l_mug scripted pick (pid_task_ctrl along build_traj_l_pick_place rows,
+    one mj_step per row).  Timed with HIP events on the library's stream, inputs resident."""
+    import torch
+    from ur3e_amd import runtime as rt
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    out = {}
+    md, mc = rt.load_model("ur3e_2f85")
+    cfg = rt.make_config(task=rt.TASK_MOVE_J, frame_skip=1, model=md, seed=3, reset_noise=False,
+                         reset_key=md["id_key_down"])
+    b = rt.Batch(mc, cfg, n_envs)
+    dev = b.obs.device
+    q0 = torch.tensor(md["key_qpos"][md["id_key_down"]][:6], dtype=torch.float64, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+
+    def act():
+        a = torch.empty((n_envs, 7), dtype=torch.float64, device=dev)
+        a[:, :6] = q0 + (torch.rand((n_envs, 6), dtype=torch.float64, device=dev, generator=g) - 0.5)
+        a[:, 6] = torch.rand(n_envs, dtype=torch.float64, device=dev, generator=g)
+        return a
+
+    def timed(step_fn):
+        for _ in range(warmup):
+            step_fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            step_fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return n_envs * steps / (e0.elapsed_time(e1) * 1e-3)
+
+    acts = [act() for _ in range(warmup + steps)]
+    it = iter(acts)
+    out["C2_ur3e_2f85_move_j"] = {"value": timed(lambda: b.step(next(it))), "unit": "env-steps/s",
+                                  "envs": n_envs, "substeps_per_env_step": 1}
+    b.close()
+    drv = MoveLMug(n_envs, reset_mode="low", seed=0)
+    rows = [drv.traj.row(t) for t in range(warmup + steps)]
+    it = iter(rows)
+    out["C3_main_move_l_mug"] = {"value": timed(lambda: drv.batch.step(next(it))), "unit": "env-steps/s",
+                                 "envs": n_envs, "substeps_per_env_step": 1}
+    drv.close()
+    return out
+
+
 def move_l_mug_parity(n_envs=512, steps=1000, seed=0):
     """Checker for the north_star's parity clause: the move_l_mug scripted grasp (C3 semantics:
     pid_task_ctrl along per-env build_traj_l_pick_place rows, one mj_step per row, 'low' mug noise)
@@ -109,6 +159,7 @@ def main():
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
     ap.add_argument("--cpu-sample-steps", type=int, default=1000)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C2/C3 secondary throughput numbers")
     ap.add_argument("--gather-self", action="store_true",
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
     args = ap.parse_args()
@@ -251,6 +302,12 @@ def main():
                           "tolerance": 1e-5}
             except Exception as e:  # the oracle is only the checker; never fail the bench on it
                 cpu = dict(value=None, unit="env-steps/s", cores=None, kind="port", sample=f"failed: {e}")
+        extra = None
+        if world == 1 and not args.no_extra:
+            try:
+                extra = other_configs(n_envs=n)
+            except Exception as e:  # secondary numbers never fail the headline line
+                extra = {"error": repr(e)}
         line = {
             "metric": "env-steps/sec at N parallel envs, 1/2/4/8 MI355X; max |qpos-ref| @1k steps",
             "value": value,
@@ -282,6 +339,7 @@ def main():
             "roofline_fp64": fp64,
             "cpu_baseline": cpu,
             "parity": parity,
+            "other_configs": extra,
         }
         print(json.dumps(line), flush=True)
     batch.close()
