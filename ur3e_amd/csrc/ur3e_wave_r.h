@@ -366,10 +366,13 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
       double ljj = sqrt(sum);
       if (lane > j) h[j] = h[j] / ljj;
       if (lane == j) h[j] = ljj;
+      /* column j to every lane through an LDS slot (broadcast reads, not a readlane per k) */
+      double* col = R_SLOT(s, j & 1);
+      r_stage(col, h[j]);
 #pragma unroll
       for (int k = j + 1; k < K_NV; k++) {
         if (k < nv) {
-          double lkj = rl(h[j], k);
+          const double lkj = col[k];
           if (lane >= k) h[k] -= h[j] * lkj;
         }
       }
@@ -413,20 +416,40 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 }
 
 /* line-search 1-D evaluation at a (w_ls_eval): per-row terms on the row lanes, ordered sums */
+/* the step-size-independent part of the cone terms, fixed for one line search: the next two rows'
+   jar / Jv (lane shuffles) and the V terms (same expressions as before, evaluated once) */
+struct RLs {
+  double jar1, jar2, Jv1, Jv2, V0, V1, V2, VV, Dm;
+};
+WD RLs r_ls_setup(const RRow& w) {
+  const int lane = w_lane();
+  RLs c;
+  c.jar1 = shf(w.jar, lane + 1); c.jar2 = shf(w.jar, lane + 2);
+  c.Jv1 = shf(w.Jv, lane + 1); c.Jv2 = shf(w.Jv, lane + 2);
+  const double mu = w.mu;
+  c.V0 = w.Jv * mu;
+  c.V1 = c.Jv1 * w.fr0;
+  c.V2 = c.Jv2 * w.fr1;
+  c.VV = 0;
+  c.VV += c.V1 * c.V1;
+  c.VV += c.V2 * c.V2;
+  c.Dm = w.D / (mu * mu * (1 + mu * mu));
+  return c;
+}
+
 template <class KS>
-WD void r_ls_eval(KS& s, const RRow& w, int nefc, double a, double gauss, double g1, double g2, double& lsF,
-                  double& lsdF, double& lsd2F) {
+WD void r_ls_eval(KS& s, const RRow& w, const RLs& c, int nefc, double a, double gauss, double g1, double g2,
+                  double& lsF, double& lsdF, double& lsd2F) {
   const int lane = w_lane();
   const double D = w.D, R = w.R;
   double x = w.jar + a * w.Jv;
   double v = w.Jv;
   /* cone terms from the contact's first row (computed everywhere, used by contact lanes) */
-  double jar1 = shf(w.jar, lane + 1), jar2 = shf(w.jar, lane + 2);
-  double Jv1 = shf(w.Jv, lane + 1), Jv2 = shf(w.Jv, lane + 2);
+  const double jar1 = c.jar1, jar2 = c.jar2, Jv1 = c.Jv1, Jv2 = c.Jv2;
   double mu = w.mu;
-  double U0 = (w.jar + a * w.Jv) * mu, V0 = w.Jv * mu;
-  double U1 = (jar1 + a * Jv1) * w.fr0, V1 = Jv1 * w.fr0;
-  double U2 = (jar2 + a * Jv2) * w.fr1, V2 = Jv2 * w.fr1;
+  double U0 = (w.jar + a * w.Jv) * mu, V0 = c.V0;
+  double U1 = (jar1 + a * Jv1) * w.fr0, V1 = c.V1;
+  double U2 = (jar2 + a * Jv2) * w.fr1, V2 = c.V2;
   double N = U0;
   double T2 = 0;
   T2 += U1 * U1;
@@ -436,10 +459,10 @@ WD void r_ls_eval(KS& s, const RRow& w, int nefc, double a, double gauss, double
   if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
   else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
   else z = 2;
-  double Dm = D / (mu * mu * (1 + mu * mu));
-  double UV = 0, VV = 0;
-  UV += U1 * V1; VV += V1 * V1;
-  UV += U2 * V2; VV += V2 * V2;
+  const double Dm = c.Dm, VV = c.VV;
+  double UV = 0;
+  UV += U1 * V1;
+  UV += U2 * V2;
   double NT_ = N - mu * T;
   double dNT = V0 - mu * UV / T;
   double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
@@ -526,7 +549,8 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   r_slot_done();
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
-  r_ls_eval(s, w, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
+  const RLs lc = r_ls_setup(w);
+  r_ls_eval(s, w, lc, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
   if (d0 >= 0) return 0;
   double lo = 0.0, dlo = d0, hlo = h0;
   double hi = -1.0, dhi = 0, hhi = 0;
@@ -535,7 +559,7 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   WT(19);
   for (int it = 0; it < m->ls_iterations; it++) {
     double f, df, d2f;
-    r_ls_eval(s, w, nefc, a, gauss, g1, g2, f, df, d2f);
+    r_ls_eval(s, w, lc, nefc, a, gauss, g1, g2, f, df, d2f);
     WT(20);
     if (f < bestF) { bestF = f; bestA = a; }
     if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
@@ -655,10 +679,13 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
       const unsigned int am = amask[k];
       if (am) {
         double tmp = a[k] / akk; /* lane i in anc(k): A[k][i] / A[k][k] */
+        /* the multipliers reach every lane through an LDS slot (broadcast reads) */
+        double* tk = R_SLOT(s, k & 1);
+        r_stage(tk, tmp);
 #pragma unroll
         for (int i = 0; i < k; i++) {
           if ((am >> i) & 1u) {
-            double ti = rl(tmp, i);
+            const double ti = tk[i];
             if ((am & lbit) && lane <= i) a[i] -= a[k] * ti;
           }
         }
