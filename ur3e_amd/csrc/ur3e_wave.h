@@ -692,7 +692,7 @@ WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
    candidate order (ballot + mbcnt), ONE narrowphase per survivor (lane = survivor), contact
    offsets by a wave prefix scan of the counts, contacts written from the lane's own results.
    Same contacts in the same order as the count / prefix / write passes of w_collision. */
-template <class KS, int VAR = 0>
+template <class KS>
 WD void r_collision(KModel m, KS& s) {
   const int lane = w_lane();
   const int np = m->ncpair;
@@ -728,7 +728,6 @@ WD void r_collision(KModel m, KS& s) {
     }
     const int off = total + incl - cnt;
     total += rli(incl, 63);
-    if constexpr (VAR == 1) continue;
     for (int k = 0; k < cnt && off + k < KS::MAXCON; k++) w_store_contact(m, s, off + k, p, raw[k]);
   }
   if (lane == 0) {
@@ -739,10 +738,10 @@ WD void r_collision(KModel m, KS& s) {
   asm volatile("" ::: "memory");
 }
 
-template <int NT, class KS, int VAR = 0>
+template <int NT, class KS>
 WD void w_collision(KModel m, KS& s) {
   if constexpr (NT == 64) {
-    r_collision<KS, VAR>(m, s);
+    r_collision<KS>(m, s);
     return;
   }
   const int tid = w_lane();
@@ -761,7 +760,6 @@ WD void w_collision(KModel m, KS& s) {
   }
   SYNC();
   if (KS::BAIL && s.ovf) return;
-  if constexpr (VAR == 1) return;
   for (int p = tid; p < np; p += NT) {
     int cnt = s.cand_count[p];
     int off = s.cand_off[p];
@@ -820,7 +818,7 @@ KD void w_row_impedance(KModel m, KS& s, int r, const double* sref, const double
   s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
 }
 
-template <int NT, class KS, int VAR = 0>
+template <int NT, class KS>
 WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
@@ -828,8 +826,7 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if constexpr (REG) {
     r_mc_layout(m, pl, s);
     if (s.ovf) return;
-    if constexpr (VAR == 1) return;
-    r_mc_rows(m, pl, s);
+      r_mc_rows(m, pl, s);
   } else {
   /* lane 0 lays out the row groups in oracle order; a group that does not fit stops the layout */
   if (tid == 0) {
@@ -867,7 +864,6 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   SYNC();
   if (KS::BAIL && s.ovf) return;
-  if constexpr (VAR == 1) return;
   /* phase A: Jacobian entries, one lane per (group, dof) */
   const int nitem = s.ngrp * nv;
   for (int it = tid; it < nitem; it += NT) {
@@ -937,7 +933,6 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   SYNC();
   }
-  if constexpr (VAR == 2) return;
   /* phase B: reference acceleration and regulariser, one lane per row */
   if constexpr (!REG)
   for (int r = tid; r < s.nefc; r += NT) {
@@ -990,7 +985,6 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   SYNC();
-  if constexpr (VAR == 3) return;
   /* phase C: elliptic regularisation per contact */
   for (int g = tid; g < s.ngrp; g += NT) {
     if (s.grp_type[g] != G_CONTACT) continue;

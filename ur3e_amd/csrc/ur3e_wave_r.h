@@ -768,8 +768,8 @@ WD void r_subtree_sum(KModel m, double (&f)[C]) {
    costs one LDS read of the parent + the arithmetic, not a chain of dependent global loads;
    bodies carry at most one joint (KPlan.max_jntnum <= 1, checked by the caller) */
 
-/* w_kinematics (mj_kinematics); VAR != 0 only in the diagnostic stage bench */
-template <class KS, int VAR = 0>
+/* w_kinematics (mj_kinematics) */
+template <class KS>
 WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
   const int nb = m->nbody, nlevel = pl->nlevel;
@@ -802,10 +802,6 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   /* hinge rotation of this body's joint (w_kinematics' qloc pass) */
   double ql[4] = {1, 0, 0, 0};
   if (depth > 0 && jn == 1 && jt != UR3E_JNT_FREE) k_axis_angle_quat(ql, jax, s.qpos[qa] - q0);
-  if constexpr (VAR == 1) {
-    if (lane < 64) s.xpos[lane % 25][0] = ql[0] + bpos[0] + jax[0] + jps[0] + bquat[0] + fpos[0] + fquat[0] + fb;
-    return;
-  }
   if (lane == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
@@ -814,11 +810,7 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   for (int lvl = 1; lvl <= nlevel; lvl++) {
-    if (VAR == 2 && depth == lvl) {
-      for (int c = 0; c < 9; c++) s.xmat[lane][c] = s.xmat[pid][c] + bpos[0];
-      for (int c = 0; c < 3; c++) s.xpos[lane][c] = s.xpos[pid][c] + jps[0];
-      for (int c = 0; c < 4; c++) s.xquat[lane][c] = s.xquat[pid][c] + ql[0];
-    } else if (depth == lvl) {
+    if (depth == lvl) {
       double xpos[3], xquat[4];
       if (jn == 1 && jt == UR3E_JNT_FREE) {
         xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
@@ -856,7 +848,6 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
-  if constexpr (VAR == 3) return;
   if (lane < nfr) {
     double bp[3], bq[4], bm[9], op[3], om[9];
     for (int c = 0; c < 3; c++) bp[c] = s.xpos[fb][c];
