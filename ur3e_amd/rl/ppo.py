@@ -5,7 +5,9 @@ gymnasium_src/scripts/regular_rl/rl/train_rl.py:60-73 with gymnasium_src/config/
 (net_arch [256, 256], lr 3e-4, batch 256, n_epochs 30, gamma 0.99, gae_lambda 0.95, ent_coef 0.01;
 SB3 defaults for the rest: clip_range 0.2, vf_coef 0.5, max_grad_norm 0.5, Adam eps 1e-5,
 normalize_advantage, state-independent log_std initialised to 0, tanh MLPs with orthogonal init).
-SB3 itself is not installed in this image; the algorithm follows stable_baselines3==2.x
+No feature extractor: train_rl.py:123 reads `hyperparameters.get("feature_encoder")` while the
+yml key is `feature_extractor`, so the reference's transformer / frame-stack branch (:26-35) is
+never taken and the policy is the plain MLP above.  SB3 itself is not installed in this image; the algorithm follows stable_baselines3==2.x
 (`PPO.train`, `OnPolicyAlgorithm.collect_rollouts`, `RolloutBuffer.compute_returns_and_advantage`).
 
 MI355X layout: the env, the on-device VecNormalize, the rollout buffer and the policy all live on
