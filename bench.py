@@ -200,6 +200,7 @@ def main():
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=1234,
                          env_id_offset=rank * n, envs_per_block=args.envs_per_block)
     batch = rt.Batch(mc, cfg, n, device=local)
+    batch_kinfo = batch.kernel_info()
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
     gen = torch.Generator(device=dev)
@@ -327,6 +328,7 @@ def main():
                                             " + full-capacity fallback", -128: "full-capacity, 128 lanes per env",
                                             -64: "full-capacity, 64 lanes per env"}.get(
                            batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),
+                       "kernel_resources": batch_kinfo,
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

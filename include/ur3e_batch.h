@@ -146,6 +146,10 @@ int ur3e_batch_nq(const ur3e_batch_t* b);
 int ur3e_batch_nv(const ur3e_batch_t* b);
 int ur3e_batch_nu(const ur3e_batch_t* b);
 
+/* the step kernel this handle launches: envs resident per CU (occupancy), static LDS bytes per
+   workgroup, registers per lane */
+int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs);
+
 /* profiling: events recorded around the most recent step kernel on its stream */
 int ur3e_batch_last_step_ms(ur3e_batch_t* b, float* ms);
 

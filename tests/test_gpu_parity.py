@@ -324,3 +324,16 @@ def test_vecnormalize_gpu_matches_sb3(norm_reward):
             np.testing.assert_array_equal(infos[i]["terminal_observation"], t)
     assert saw_done
     vn.close()
+
+
+@pytest.mark.gpu
+def test_compact_kernel_occupancy():
+    """the main.xml compact tier must keep eight envs per CU (20 KB LDS, <= 256 registers): a change
+    that grows the LDS layout or the register count silently halves throughput otherwise"""
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model("main")
+    b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1), 64)
+    info = b.kernel_info()
+    b.close()
+    assert info["lds_bytes"] <= 20480, info
+    assert info["envs_per_cu"] >= 8, info

@@ -1526,6 +1526,36 @@ extern "C" int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream
   return UR3E_OK;
 }
 
+/* resources and occupancy of the step kernel this handle launches (the dominant kernel) */
+extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(b->device));
+  const void* fn;
+  int nt;
+  if (b->tiered) {
+    nt = 64;
+    fn = b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
+  } else if (b->wave_nt == 128) {
+    nt = 128;
+    fn = (const void*)w_env_step<128, KSL>;
+  } else if (b->wave_nt == 64) {
+    nt = 64;
+    fn = (const void*)w_env_step<64, KSL>;
+  } else {
+    nt = 64;
+    fn = (const void*)k_env_step;
+  }
+  hipFuncAttributes attr;
+  HIPCHK(hipFuncGetAttributes(&attr, fn));
+  int blocks = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, nt, 0));
+  const int envs = (b->tiered || b->wave_nt) ? blocks : blocks * nt; /* v1: one env per lane */
+  if (envs_per_cu) *envs_per_cu = envs;
+  if (lds_bytes) *lds_bytes = (int)attr.sharedSizeBytes;
+  if (regs) *regs = attr.numRegs;
+  return UR3E_OK;
+}
+
 /* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */
 extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {
 #ifdef UR3E_STAGE_TIMING

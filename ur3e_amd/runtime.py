@@ -238,6 +238,12 @@ class Batch:
         _check(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
         return int(v.value)
 
+    def kernel_info(self) -> dict:
+        """{envs_per_cu, lds_bytes, regs} of the step kernel this handle launches"""
+        e, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
+        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value}
+
     def last_step_ms(self) -> float:
         ms = ctypes.c_float()
         _check(self.L.ur3e_batch_last_step_ms(self.h, ctypes.byref(ms)))
