@@ -92,6 +92,11 @@ def test_ppo_iteration_and_timeout_bootstrap():
     raw_mean = algo.buf_rew[:4].mean().item()
     assert np.isfinite(raw_mean)
     assert torch.all(algo.buf_start[5] == 1) and torch.all(algo.buf_start[0] == 1)
+    # rollout-time log-probabilities and values equal a fresh evaluation of the stored (obs, action)
+    with torch.no_grad():
+        v, logp, _ = algo.policy.evaluate(algo.buf_obs.reshape(48, -1), algo.buf_act.reshape(48, -1))
+    np.testing.assert_allclose(logp.numpy(), algo.buf_logp.reshape(-1).numpy(), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(v.numpy(), algo.buf_val.reshape(-1).numpy(), rtol=1e-5, atol=1e-5)
     before = [p.detach().clone() for p in algo.policy.parameters()]
     algo.train()
     assert all(np.isfinite(v) for v in algo.stats.values())

@@ -1,17 +1,17 @@
 /* On-device SB3 VecNormalize (include/ur3e_vecnorm.h): running observation / return statistics in
  * numpy's exact reduction order, then normalisation.
  *
- * k_vn_stats (one workgroup, two wavefronts):
- *   wave 0, lane j < dim: column j of obs [n, dim]: mean = (((x0 + x1) + x2) + ...) / n and
- *     var = sum((x - mean)^2) / n in the same row-sequential order numpy uses for an axis-0
- *     reduction of a C-contiguous array, then RunningMeanStd.update_from_moments;
- *   wave 1: returns = returns * gamma + reward (all lanes), then lane 0 runs numpy's pairwise
+ * k_vn_stats (two workgroups of 1024 threads on two CUs, rows staged through LDS):
+ *   block 1: returns = returns * gamma + reward (all threads), then thread 0 runs numpy's pairwise
  *     summation (8 accumulators per <=128 block, halves rounded down to multiples of 8) for the
- *     1-D mean and var of the returns.
+ *     1-D mean and var of the returns;
+ *   block 0, thread j < dim: column j of obs [n, dim]: mean = (((x0 + x1) + x2) + ...) / n and
+ *     var = sum((x - mean)^2) / n in the same row-sequential order numpy uses for an axis-0
+ *     reduction of a C-contiguous array, then RunningMeanStd.update_from_moments.
  * k_vn_apply (n x dim threads): obs / terminal-obs normalisation to f32, reward normalisation,
  *   returns[done] = 0.
- * Both are tiny next to the env step (~30 us of dependent FP64 adds at n = 4096); the bound is the
- * serial order SB3 fixes, not bandwidth. */
+ * The bound is the serial order SB3 fixes (~8k dependent FP64 adds per column at n = 4096), so the
+ * loads are staged into LDS by the whole workgroup and kept off the add chains. */
 #include <hip/hip_runtime.h>
 
 #include "../../include/ur3e_batch.h"
@@ -92,48 +92,86 @@ __device__ static void vn_moments(double* mean, double* var, double c, double bm
   *var = new_var;
 }
 
-__global__ __launch_bounds__(128) void k_vn_stats(ur3e_vecnorm_stats_t st, int n, int dim, const double* __restrict__ obs,
-                                                  const double* __restrict__ rew, int upd_obs, int upd_ret,
-                                                  double gamma, int reset) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+/* One workgroup of VN_NT threads.  The serial orders are fixed by numpy, so the work here is keeping
+   the loads off the dependent add chains: the whole workgroup stages row chunks of obs (and the
+   returns) into LDS with coalesced loads, then the lanes that own a column (obs) or lane 0
+   (returns, pairwise) walk LDS in numpy's order. */
+#define VN_NT 1024
+#define VN_LDS_DOUBLES 12288 /* 96 KB of obs rows per chunk */
+#define VN_RET_LDS 4096      /* returns staged in LDS when n <= this (32 KB) */
+__global__ __launch_bounds__(VN_NT) void k_vn_stats(ur3e_vecnorm_stats_t st, int n, int dim,
+                                                    const double* __restrict__ obs, const double* __restrict__ rew,
+                                                    int upd_obs, int upd_ret, double gamma, int reset) {
+  __shared__ double buf[VN_LDS_DOUBLES];
+  __shared__ double rbuf[VN_RET_LDS];
+  const int tid = threadIdx.x;
   const double bn = (double)n;
-  if (wave == 0) {
-    if (!upd_obs) return;
-    const double c = *st.obs_count;
-    if (lane < dim) {
-      const int j = lane;
-      /* np.mean / np.var over axis 0 of a C-contiguous [n, dim]: row-sequential per column */
-      double s = obs[j];
-      for (int i = 1; i < n; i++) s = s + obs[(size_t)i * dim + j];
-      const double bm = s / bn;
-      double d0 = obs[j] - bm;
-      double q = d0 * d0;
-      for (int i = 1; i < n; i++) {
-        const double d = obs[(size_t)i * dim + j] - bm;
-        q = q + d * d;
-      }
-      vn_moments(st.obs_mean + j, st.obs_var + j, c, bm, q / bn, bn);
-    }
-    if (lane == 0) *st.obs_count = bn + c;
-    return;
-  }
-  /* wave 1: discounted returns and their statistics (1-D: numpy pairwise summation) */
+  /* block 1: discounted returns and their statistics (1-D: numpy pairwise summation); block 0: the
+     observation columns -- independent, so they run on two CUs at once */
+  if (blockIdx.x == 1) {
   if (reset) {
-    for (int i = lane; i < n; i += 64) st.returns[i] = 0.0;
-    return;
+    for (int i = tid; i < n; i += VN_NT) st.returns[i] = 0.0;
+  } else if (upd_ret) {
+    const bool in_lds = n <= VN_RET_LDS;
+    for (int i = tid; i < n; i += VN_NT) {
+      const double r = st.returns[i] * gamma + rew[i];
+      st.returns[i] = r;
+      if (in_lds) rbuf[i] = r;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) {
+      const double* a = in_lds ? rbuf : st.returns;
+      const double bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
+      const double q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+      const double c = *st.ret_count;
+      vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);
+      *st.ret_count = bn + c;
+    }
   }
-  if (!upd_ret) return;
-  for (int i = lane; i < n; i += 64) st.returns[i] = st.returns[i] * gamma + rew[i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane != 0) return;
-  const double* a = st.returns;
-  const double bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
-  const double q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
-  const double c = *st.ret_count;
-  vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);
-  *st.ret_count = bn + c;
+  return;
+  }
+  if (!upd_obs) return;
+  /* ---- observation columns: np.mean / np.var over axis 0 of a C-contiguous [n, dim], row-sequential
+     per column; two sweeps (sum, then squared deviations from the batch mean) ---- */
+  const int rows = VN_LDS_DOUBLES / dim;
+  const int j = tid;
+  double s = 0.0, bm = 0.0, q = 0.0;
+  for (int pass = 0; pass < 2; pass++) {
+    for (int base = 0; base < n; base += rows) {
+      const int nr = n - base < rows ? n - base : rows;
+      __syncthreads();
+      const size_t off = (size_t)base * dim;
+      for (int k = tid; k < nr * dim; k += VN_NT) buf[k] = obs[off + k];
+      __syncthreads();
+      if (j < dim) {
+        int i0 = 0;
+        if (base == 0) { /* numpy starts each column from its first element */
+          if (pass == 0) {
+            s = buf[j];
+          } else {
+            const double d0 = buf[j] - bm;
+            q = d0 * d0;
+          }
+          i0 = 1;
+        }
+        if (pass == 0) {
+#pragma unroll 8
+          for (int i = i0; i < nr; i++) s = s + buf[i * dim + j];
+        } else {
+#pragma unroll 8
+          for (int i = i0; i < nr; i++) {
+            const double d = buf[i * dim + j] - bm;
+            q = q + d * d;
+          }
+        }
+      }
+    }
+    if (pass == 0) bm = s / bn;
+  }
+  if (j < dim) vn_moments(st.obs_mean + j, st.obs_var + j, *st.obs_count, bm, q / bn, bn);
+  __syncthreads(); /* every column read the old count before it is replaced */
+  if (tid == 0) *st.obs_count = bn + *st.obs_count;
 }
 
 __device__ static inline float vn_norm(double x, double mean, double var, double eps, double clip) {
@@ -188,7 +226,7 @@ extern "C" int ur3e_vecnorm_step(const ur3e_vecnorm_stats_t* st, const ur3e_vecn
   if (rc) return rc;
   if (!d_rew || !d_term || !d_trunc) return ur3e_internal_fail(UR3E_EINVAL, "null reward / done buffer");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_vn_stats, dim3(1), dim3(128), 0, s, *st, n, dim, d_obs, d_rew, cfg->training && cfg->norm_obs,
+  hipLaunchKernelGGL(k_vn_stats, dim3(2), dim3(VN_NT), 0, s, *st, n, dim, d_obs, d_rew, cfg->training && cfg->norm_obs,
                      cfg->training, cfg->gamma, 0);
   VN_CHK(hipGetLastError());
   hipLaunchKernelGGL(k_vn_apply, dim3((n * dim + 255) / 256), dim3(256), 0, s, *st, n, dim, d_obs, d_rew, d_term,
@@ -203,7 +241,7 @@ extern "C" int ur3e_vecnorm_reset(const ur3e_vecnorm_stats_t* st, const ur3e_vec
   int rc = vn_check(st, cfg, n, dim, d_obs);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_vn_stats, dim3(1), dim3(128), 0, s, *st, n, dim, d_obs, nullptr, cfg->training && cfg->norm_obs,
+  hipLaunchKernelGGL(k_vn_stats, dim3(2), dim3(VN_NT), 0, s, *st, n, dim, d_obs, nullptr, cfg->training && cfg->norm_obs,
                      0, cfg->gamma, 1);
   VN_CHK(hipGetLastError());
   hipLaunchKernelGGL(k_vn_apply, dim3((n * dim + 255) / 256), dim3(256), 0, s, *st, n, dim, d_obs, nullptr, nullptr,

@@ -128,26 +128,29 @@ class PPO:
 
     # -- rollout ---------------------------------------------------------------
     def _rollout_step(self, t: int):
-        """One env step at rollout index t (persistent tensors; no host synchronisation)."""
+        """One env step at rollout index t (persistent tensors; no host synchronisation).
+        Launch count is what limits a 4,096-env rollout step, so: the sampling noise and the
+        log-probabilities are handled for the whole rollout at once (log_std is constant during a
+        rollout: log N(mean + std*eps) = -eps^2/2 - log_std - log(2 pi)/2), and the value of the next
+        observation and of the terminal observation share one critic pass over 2N rows."""
+        N = self.n_envs
         obs = self._obs
-        d = self.policy.dist(obs)
-        act = d.mean + d.stddev * self._noise[t]
-        val = self.policy.value(obs)
-        logp = d.log_prob(act).sum(-1)
+        act = self.policy.action_net(self.policy.pi_net(obs)) + self._std * self._noise[t]
         clipped = torch.maximum(torch.minimum(act, self.high), self.low)
         nobs, rew, term, trunc, tobs = self.env.step_torch(clipped.to(torch.float64))
-        rew = rew.to(torch.float32)
+        self._vin[:N].copy_(nobs)
+        self._vin[N:].copy_(tobs)
+        v2 = self.policy.value(self._vin)
         term, trunc = term.bool(), trunc.bool()
         # SB3 timeout bootstrap: truncated-not-terminated envs get gamma * V(terminal obs); evaluated
         # for every env and masked, so the rollout never waits on the host for an any()
-        boot = trunc & ~term
-        rew = rew + self.gamma * torch.where(boot, self.policy.value(tobs.to(torch.float32)), torch.zeros_like(rew))
+        rew = rew.to(torch.float32) + self.gamma * torch.where(trunc & ~term, v2[N:], torch.zeros_like(v2[N:]))
         self.buf_obs[t].copy_(obs)
         self.buf_act[t].copy_(act)
         self.buf_rew[t].copy_(rew)
         self.buf_start[t].copy_(self._start)
-        self.buf_val[t].copy_(val)
-        self.buf_logp[t].copy_(logp)
+        self.buf_val[t].copy_(self._val)
+        self._val.copy_(v2[:N])
         self._obs.copy_(nobs)  # the env reuses its output buffers: copy, never alias
         self._start.copy_((term | trunc).to(torch.float32))
 
@@ -155,11 +158,18 @@ class PPO:
     def collect_rollouts(self):
         if self._obs is None:
             self._obs = self.env.reset_torch().to(torch.float32).clone()
+            self._val = self.policy.value(self._obs)
+            self._vin = torch.empty((2 * self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+        else:  # the critic changed in train(): value the carried-over observation with the new one
+            self._val = self.policy.value(self._obs)
         # all sampling noise of the rollout in one draw
         self._noise.normal_(generator=self.gen)
+        self._std = self.policy.log_std.exp()
         for t in range(self.n_steps):
             self._rollout_step(t)
-        last_val = self.policy.value(self._obs)
+        ls = self.policy.log_std
+        self.buf_logp.copy_(-0.5 * self._noise.pow(2).sum(-1) - (ls.sum() + 0.5 * math.log(2 * math.pi) * ls.numel()))
+        last_val = self._val
         self.adv, self.ret = compute_gae(self.buf_rew, self.buf_val, self.buf_start, last_val, self._start > 0,
                                          self.gamma, self.lam)
         self.num_timesteps += self.n_steps * self.n_envs
