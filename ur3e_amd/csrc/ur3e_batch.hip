@@ -40,14 +40,27 @@
 KD void k_quat_from_matrix(const double mt[9], double q[4]) {
   double dec[4] = {mt[0], mt[4], mt[8], mt[0] + mt[4] + mt[8]};
   int ch = 0;
+  double dch = dec[0];
+#pragma unroll
   for (int k = 1; k < 4; k++)
-    if (dec[k] > dec[ch]) ch = k;
-  if (ch != 3) {
-    int i = ch, j = (i + 1) % 3, k = (j + 1) % 3;
-    q[i] = 1 - dec[3] + 2 * mt[3 * i + i];
-    q[j] = mt[3 * j + i] + mt[3 * i + j];
-    q[k] = mt[3 * k + i] + mt[3 * i + k];
-    q[3] = mt[3 * k + j] - mt[3 * j + k];
+    if (dec[k] > dch) { ch = k; dch = dec[k]; }
+  /* i = ch, j = (i + 1) % 3, k = (j + 1) % 3 spelt out per case (constant indices: no private
+     array indexed at run time) */
+  if (ch == 0) {
+    q[0] = 1 - dec[3] + 2 * mt[0];
+    q[1] = mt[3] + mt[1];
+    q[2] = mt[6] + mt[2];
+    q[3] = mt[7] - mt[5];
+  } else if (ch == 1) {
+    q[1] = 1 - dec[3] + 2 * mt[4];
+    q[2] = mt[7] + mt[5];
+    q[0] = mt[1] + mt[3];
+    q[3] = mt[2] - mt[6];
+  } else if (ch == 2) {
+    q[2] = 1 - dec[3] + 2 * mt[8];
+    q[0] = mt[2] + mt[6];
+    q[1] = mt[5] + mt[7];
+    q[3] = mt[3] - mt[1];
   } else {
     q[0] = mt[7] - mt[5];
     q[1] = mt[2] - mt[6];
@@ -938,9 +951,13 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       }
       if (m->nu > 6) ctrl[6] = o.a[6] * m->act_ctrlrange[m->nu - 1][1];
     } else {
-      for (int k = 0; k < m->nu; k++) ctrl[k] = o.a[k];
+#pragma unroll
+      for (int k = 0; k < K_NU; k++)
+        if (k < m->nu) ctrl[k] = o.a[k];
     }
-    for (int k = 0; k < m->nu; k++) s.ctrl[k] = ctrl[k];
+#pragma unroll
+    for (int k = 0; k < K_NU; k++)
+      if (k < m->nu) s.ctrl[k] = ctrl[k];
   }
   SYNC();
   const int fs = (k_is_gym(c.task) || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;

@@ -569,8 +569,38 @@ KD void k_make_frame(double f[9], const double n[3]) {
   k_frame_rest(f);
 }
 
-KD int k_plane_box(const double pp[3], const double pm[9], const double bp[3], const double bm[9],
-                   const double bs[3], double margin, KRaw* out) {
+/* Narrowphase routines are templated on where their intermediate polygons live (Clip) and where
+   their contacts go (Emit), so the compact tier can keep both in LDS (dynamic indices there are
+   plain ds_read/ds_write addresses) while the other tiers keep private arrays.  The arithmetic and
+   its order are the same for every instantiation.
+     Clip: double get(int buf, int v, int c) / void set(int buf, int v, int c, double x),
+           buf in {0, 1} (ping-pong), v < 8, c < 3
+     Emit: void operator()(int k, const double pos[3], const double n[3], double dist) */
+struct KRawEmit {
+  KRaw* out;
+  __device__ __forceinline__ void operator()(int k, const double pos[3], const double n[3], double dist) const {
+    out[k].pos[0] = pos[0]; out[k].pos[1] = pos[1]; out[k].pos[2] = pos[2];
+    out[k].n[0] = n[0]; out[k].n[1] = n[1]; out[k].n[2] = n[2];
+    out[k].dist = dist;
+  }
+};
+struct KPrivClip {
+  double b[2][8][3];
+  __device__ __forceinline__ double get(int buf, int v, int c) const { return b[buf][v][c]; }
+  __device__ __forceinline__ void set(int buf, int v, int c, double x) { b[buf][v][c] = x; }
+};
+
+/* column i (i in 0..2, may be lane-varying) of a row-major 3x3 matrix read straight from where the
+   matrix lives (LDS / global): the frame axes of the box-box test without a dynamically indexed
+   private array */
+__device__ __forceinline__ void k_col3(double out[3], const double* R, int i) {
+  out[0] = R[i]; out[1] = R[3 + i]; out[2] = R[6 + i];
+}
+
+template <class Emit>
+__device__ static __forceinline__ int k_plane_box_t(const double pp[3], const double pm[9], const double bp[3],
+                                                     const double bm[9], const double bs[3], double margin,
+                                                     const Emit& emit) {
   double n[3] = {pm[2], pm[5], pm[8]};
   double dif[3] = {bp[0] - pp[0], bp[1] - pp[1], bp[2] - pp[2]};
   double dist = k_dot3(n, dif);
@@ -581,22 +611,26 @@ KD int k_plane_box(const double pp[3], const double pm[9], const double bp[3], c
     k_mat_vec3(corner, bm, v);
     double ld = k_dot3(n, corner);
     if (dist + ld > margin || ld > 0) continue;
-    KRaw* c = out + cnt;
-    c->dist = dist + ld;
-    c->n[0] = n[0]; c->n[1] = n[1]; c->n[2] = n[2];
-    double h = c->dist * 0.5;
-    c->pos[0] = corner[0] - n[0] * h + bp[0];
-    c->pos[1] = corner[1] - n[1] * h + bp[1];
-    c->pos[2] = corner[2] - n[2] * h + bp[2];
+    const double cd = dist + ld;
+    double h = cd * 0.5;
+    double pos[3] = {corner[0] - n[0] * h + bp[0], corner[1] - n[1] * h + bp[1], corner[2] - n[2] * h + bp[2]};
+    emit(cnt, pos, n, cd);
     if (++cnt >= 4) return cnt;
   }
   return cnt;
 }
 
-__device__ static __forceinline__ int k_box_box_inl(const double p1[3], const double R1[9], const double s1[3],
-                                                     const double p2[3], const double R2[9], const double s2[3],
-                                                     double margin, KRaw* out) {
+KD int k_plane_box(const double pp[3], const double pm[9], const double bp[3], const double bm[9],
+                   const double bs[3], double margin, KRaw* out) {
+  return k_plane_box_t(pp, pm, bp, bm, bs, margin, KRawEmit{out});
+}
+
+template <class Clip, class Emit>
+__device__ static __forceinline__ int k_box_box_t(const double p1[3], const double R1[9], const double s1[3],
+                                                   const double p2[3], const double R2[9], const double s2[3],
+                                                   double margin, Clip& clip, const Emit& emit) {
   double a[3][3], b[3][3];
+#pragma unroll
   for (int k = 0; k < 3; k++) {
     a[k][0] = R1[k]; a[k][1] = R1[3 + k]; a[k][2] = R1[6 + k];
     b[k][0] = R2[k]; b[k][1] = R2[3 + k]; b[k][2] = R2[6 + k];
@@ -605,10 +639,13 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
   double best = -1e300;
   int bestcode = -1;
   double bestax[3] = {0, 0, 0};
+#pragma unroll
   for (int code = 0; code < 6; code++) {
     const double* ax = code < 3 ? a[code] : b[code - 3];
     double ext = 0;
+#pragma unroll
     for (int k = 0; k < 3; k++) ext += s1[k] * fabs(k_dot3(a[k], ax));
+#pragma unroll
     for (int k = 0; k < 3; k++) ext += s2[k] * fabs(k_dot3(b[k], ax));
     double s = fabs(k_dot3(pp, ax)) - ext;
     if (s > margin) return 0;
@@ -617,7 +654,9 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
       bestax[0] = ax[0]; bestax[1] = ax[1]; bestax[2] = ax[2];
     }
   }
+#pragma unroll
   for (int i = 0; i < 3; i++) {
+#pragma unroll
     for (int j = 0; j < 3; j++) {
       double u[3];
       k_cross3(u, a[i], b[j]);
@@ -625,7 +664,9 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
       if (len < 1e-6) continue;
       u[0] /= len; u[1] /= len; u[2] /= len;
       double ext = 0;
+#pragma unroll
       for (int k = 0; k < 3; k++) ext += s1[k] * fabs(k_dot3(a[k], u));
+#pragma unroll
       for (int k = 0; k < 3; k++) ext += s2[k] * fabs(k_dot3(b[k], u));
       double s = fabs(k_dot3(pp, u)) - ext;
       if (s > margin) return 0;
@@ -640,7 +681,11 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
 
   if (bestcode >= 6) {
     int i = (bestcode - 6) / 3, j = (bestcode - 6) % 3;
+    double ai[3], bj[3];
+    k_col3(ai, R1, i);
+    k_col3(bj, R2, j);
     double pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+#pragma unroll
     for (int k = 0; k < 3; k++) {
       if (k != i) {
         double sg = k_dot3(n, a[k]) > 0 ? 1.0 : -1.0;
@@ -652,21 +697,18 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
       }
     }
     double w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
-    double uaub = k_dot3(a[i], b[j]);
-    double q1 = k_dot3(a[i], w), q2 = k_dot3(b[j], w);
+    double uaub = k_dot3(ai, bj);
+    double q1 = k_dot3(ai, w), q2 = k_dot3(bj, w);
     double den = 1.0 - uaub * uaub;
     double t = 0, u = 0;
     if (den > 1e-12) {
       t = (uaub * q2 - q1) / den;
       u = (q2 - uaub * q1) / den;
     }
-    double ca[3] = {pa[0] + t * a[i][0], pa[1] + t * a[i][1], pa[2] + t * a[i][2]};
-    double cb[3] = {pb[0] + u * b[j][0], pb[1] + u * b[j][1], pb[2] + u * b[j][2]};
-    out[0].pos[0] = 0.5 * (ca[0] + cb[0]);
-    out[0].pos[1] = 0.5 * (ca[1] + cb[1]);
-    out[0].pos[2] = 0.5 * (ca[2] + cb[2]);
-    out[0].n[0] = n[0]; out[0].n[1] = n[1]; out[0].n[2] = n[2];
-    out[0].dist = best;
+    double ca[3] = {pa[0] + t * ai[0], pa[1] + t * ai[1], pa[2] + t * ai[2]};
+    double cb[3] = {pb[0] + u * bj[0], pb[1] + u * bj[1], pb[2] + u * bj[2]};
+    double pos[3] = {0.5 * (ca[0] + cb[0]), 0.5 * (ca[1] + cb[1]), 0.5 * (ca[2] + cb[2])};
+    emit(0, pos, n, best);
     return 1;
   }
 
@@ -676,77 +718,97 @@ __device__ static __forceinline__ int k_box_box_inl(const double p1[3], const do
   const double* ip = ref_is_1 ? p2 : p1;
   const double* rs = ref_is_1 ? s1 : s2;
   const double* is = ref_is_1 ? s2 : s1;
-  double ra[3][3], ia[3][3];
-  for (int k = 0; k < 3; k++)
-    for (int c = 0; c < 3; c++) {
-      ra[k][c] = ref_is_1 ? a[k][c] : b[k][c];
-      ia[k][c] = ref_is_1 ? b[k][c] : a[k][c];
-    }
+  const double* rR = ref_is_1 ? R1 : R2; /* ra[k] = column k of rR */
+  const double* iR = ref_is_1 ? R2 : R1; /* ia[k] = column k of iR */
   double nr[3] = {ref_is_1 ? n[0] : -n[0], ref_is_1 ? n[1] : -n[1], ref_is_1 ? n[2] : -n[2]};
-  double rsg = k_dot3(nr, ra[fk]) > 0 ? 1.0 : -1.0;
-  double cr[3] = {rp[0] + rsg * rs[fk] * ra[fk][0], rp[1] + rsg * rs[fk] * ra[fk][1],
-                  rp[2] + rsg * rs[fk] * ra[fk][2]};
+  double rafk[3];
+  k_col3(rafk, rR, fk);
+  const double rsfk = rs[fk];
+  double rsg = k_dot3(nr, rafk) > 0 ? 1.0 : -1.0;
+  double cr[3] = {rp[0] + rsg * rsfk * rafk[0], rp[1] + rsg * rsfk * rafk[1], rp[2] + rsg * rsfk * rafk[2]};
   int t1 = (fk + 1) % 3, t2 = (fk + 2) % 3;
+  double rat1[3], rat2[3];
+  k_col3(rat1, rR, t1);
+  k_col3(rat2, rR, t2);
+  const double rst1 = rs[t1], rst2 = rs[t2];
   int im = 0;
   double bd = -1;
-  double dm[3];
+#pragma unroll
   for (int k = 0; k < 3; k++) {
-    dm[k] = k_dot3(ia[k], nr);
-    if (fabs(dm[k]) > bd) { bd = fabs(dm[k]); im = k; }
+    double iak[3];
+    k_col3(iak, iR, k);
+    const double dmk = k_dot3(iak, nr);
+    if (fabs(dmk) > bd) { bd = fabs(dmk); im = k; }
   }
-  double isg = dm[im] > 0 ? -1.0 : 1.0;
-  double ic[3] = {ip[0] + isg * is[im] * ia[im][0], ip[1] + isg * is[im] * ia[im][1],
-                  ip[2] + isg * is[im] * ia[im][2]};
+  double iaim[3], iau1[3], iau2[3];
+  k_col3(iaim, iR, im);
+  const double dmim = k_dot3(iaim, nr); /* = dm[im], recomputed from the same operands */
+  double isg = dmim > 0 ? -1.0 : 1.0;
+  const double isim = is[im];
+  double ic[3] = {ip[0] + isg * isim * iaim[0], ip[1] + isg * isim * iaim[1], ip[2] + isg * isim * iaim[2]};
   int u1 = (im + 1) % 3, u2 = (im + 2) % 3;
+  k_col3(iau1, iR, u1);
+  k_col3(iau2, iR, u2);
+  const double isu1 = is[u1], isu2 = is[u2];
   /* a quad clipped by the 4 half-planes of a rectangle never exceeds 8 vertices (each clip adds
-     at most one), so 8-point buffers hold every intermediate polygon */
-  double poly[8][3], tmp[8][3];
+     at most one), so 8-point buffers hold every intermediate polygon; clip e reads buffer e & 1
+     and writes the other one */
   int np = 4;
   const double sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     double v[3];
-    for (int c = 0; c < 3; c++) v[c] = ic[c] + sx[k] * is[u1] * ia[u1][c] + sy[k] * is[u2] * ia[u2][c] - cr[c];
-    poly[k][0] = k_dot3(v, ra[t1]);
-    poly[k][1] = k_dot3(v, ra[t2]);
-    poly[k][2] = k_dot3(v, nr);
+#pragma unroll
+    for (int c = 0; c < 3; c++) v[c] = ic[c] + sx[k] * isu1 * iau1[c] + sy[k] * isu2 * iau2[c] - cr[c];
+    clip.set(0, k, 0, k_dot3(v, rat1));
+    clip.set(0, k, 1, k_dot3(v, rat2));
+    clip.set(0, k, 2, k_dot3(v, nr));
   }
+#pragma unroll
   for (int e = 0; e < 4; e++) {
-    int ax = e >> 1;
+    const int ax = e >> 1, src = e & 1, dst = src ^ 1;
     double sgn = (e & 1) ? -1.0 : 1.0;
-    double lim = ax == 0 ? rs[t1] : rs[t2];
+    double lim = ax == 0 ? rst1 : rst2;
     int nn = 0;
     for (int k = 0; k < np; k++) {
-      const double* P = poly[k];
-      const double* Q = poly[(k + 1) % np];
+      const int kq = k + 1 < np ? k + 1 : 0;
+      double P[3] = {clip.get(src, k, 0), clip.get(src, k, 1), clip.get(src, k, 2)};
+      double Q[3] = {clip.get(src, kq, 0), clip.get(src, kq, 1), clip.get(src, kq, 2)};
       double dp = sgn * P[ax] - lim, dq = sgn * Q[ax] - lim;
       if (dp <= 0) {
-        tmp[nn][0] = P[0]; tmp[nn][1] = P[1]; tmp[nn][2] = P[2];
+        clip.set(dst, nn, 0, P[0]); clip.set(dst, nn, 1, P[1]); clip.set(dst, nn, 2, P[2]);
         nn++;
       }
       if ((dp <= 0) != (dq <= 0)) {
         double tt = dp / (dp - dq);
-        tmp[nn][0] = P[0] + tt * (Q[0] - P[0]);
-        tmp[nn][1] = P[1] + tt * (Q[1] - P[1]);
-        tmp[nn][2] = P[2] + tt * (Q[2] - P[2]);
+        clip.set(dst, nn, 0, P[0] + tt * (Q[0] - P[0]));
+        clip.set(dst, nn, 1, P[1] + tt * (Q[1] - P[1]));
+        clip.set(dst, nn, 2, P[2] + tt * (Q[2] - P[2]));
         nn++;
       }
     }
     np = nn;
-    for (int k = 0; k < np; k++) { poly[k][0] = tmp[k][0]; poly[k][1] = tmp[k][1]; poly[k][2] = tmp[k][2]; }
     if (np == 0) break;
   }
+  /* after the fourth clip the polygon is in buffer 0 (np == 0 after an early break) */
   int cnt = 0;
   for (int k = 0; k < np && cnt < 8; k++) {
-    double h = poly[k][2];
+    const double x = clip.get(0, k, 0), y = clip.get(0, k, 1), h = clip.get(0, k, 2);
     if (h > margin) continue;
     double w[3];
-    for (int c = 0; c < 3; c++) w[c] = cr[c] + poly[k][0] * ra[t1][c] + poly[k][1] * ra[t2][c] + (h * 0.5) * nr[c];
-    out[cnt].pos[0] = w[0]; out[cnt].pos[1] = w[1]; out[cnt].pos[2] = w[2];
-    out[cnt].n[0] = n[0]; out[cnt].n[1] = n[1]; out[cnt].n[2] = n[2];
-    out[cnt].dist = h;
+#pragma unroll
+    for (int c = 0; c < 3; c++) w[c] = cr[c] + x * rat1[c] + y * rat2[c] + (h * 0.5) * nr[c];
+    emit(cnt, w, n, h);
     cnt++;
   }
   return cnt;
+}
+
+__device__ static __forceinline__ int k_box_box_inl(const double p1[3], const double R1[9], const double s1[3],
+                                                     const double p2[3], const double R2[9], const double s2[3],
+                                                     double margin, KRaw* out) {
+  KPrivClip clip;
+  return k_box_box_t(p1, R1, s1, p2, R2, s2, margin, clip, KRawEmit{out});
 }
 
 /* out-of-line copy for the multi-call-site paths (keeps those kernels' code size down) */

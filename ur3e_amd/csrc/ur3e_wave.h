@@ -28,6 +28,10 @@
 
 #define W_MAXCAND 128 /* collision candidates handled per env (main.xml: 92) */
 #define W_MAXGRP 96   /* constraint row groups */
+/* compact-tier narrowphase: survivor lanes per chunk (their clip polygons live in LDS) and staged
+   raw contacts per chunk (>= the compact tier's MAXCON: a chunk staging more has overflowed) */
+#define W_NP_LANES 16
+#define W_NP_STAGE 16
 
 /* host-precomputed tree bookkeeping for the cooperative stages */
 struct KPlan {
@@ -187,6 +191,13 @@ struct KSX<MC, ME, NVC, TREE, true> {
               double b6[K_NB][6];
             } body;
           } u;
+        };
+        struct { /* KN, collision: clip polygons of one chunk of survivor lanes ([buf][vertex][coord]
+                    [lane], conflict-free across lanes) and that chunk's staged raw contacts */
+          double np_clip[2][8][3][W_NP_LANES];
+          double np_stage[7][W_NP_STAGE]; /* pos[3], n[3], dist */
+          int np_key[W_NP_STAGE];         /* survivor lane * 8 + contact index within the lane */
+          int np_nstage;
         };
       };
     };
@@ -664,6 +675,52 @@ WD int w_narrow_core(KModel m, const KS& s, int p, KRaw* raw) {
   return 0;
 }
 
+/* compact tier: clip polygons in LDS (lane ln of the chunk) and contacts staged in LDS through an
+   LDS counter, keyed by (lane, index) so that the copy pass can place them in candidate order */
+struct KLdsClip {
+  double* base;
+  int ln;
+  __device__ __forceinline__ double get(int buf, int v, int c) const {
+    return base[((buf * 8 + v) * 3 + c) * W_NP_LANES + ln];
+  }
+  __device__ __forceinline__ void set(int buf, int v, int c, double x) {
+    base[((buf * 8 + v) * 3 + c) * W_NP_LANES + ln] = x;
+  }
+};
+struct KStageEmit {
+  double* st;
+  int* key;
+  int* nst;
+  int ln;
+  __device__ __forceinline__ void operator()(int k, const double pos[3], const double n[3], double dist) const {
+    const int slot = atomicAdd(nst, 1);
+    if (slot < W_NP_STAGE) {
+      st[0 * W_NP_STAGE + slot] = pos[0]; st[1 * W_NP_STAGE + slot] = pos[1]; st[2 * W_NP_STAGE + slot] = pos[2];
+      st[3 * W_NP_STAGE + slot] = n[0]; st[4 * W_NP_STAGE + slot] = n[1]; st[5 * W_NP_STAGE + slot] = n[2];
+      st[6 * W_NP_STAGE + slot] = dist;
+      key[slot] = ln * 8 + k;
+    }
+  }
+};
+
+/* w_narrow_core with the compact tier's LDS clip buffers and contact stage (lane ln < W_NP_LANES) */
+template <class KS>
+WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
+  int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
+  double margin = m->cpair_margin[p];
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const KStageEmit emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
+  if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
+    return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2],
+                         margin, emit);
+  if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX) {
+    KLdsClip clip{&s.np_clip[0][0][0][0], ln};
+    return k_box_box_t(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
+                       m->geom_size[g2], margin, clip, emit);
+  }
+  return 0;
+}
+
 template <class KS>
 WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
   return w_pair_near(m, s, p) ? w_narrow_core(m, s, p, raw) : 0;
@@ -708,6 +765,59 @@ WD void r_collision(KModel m, KS& s) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   int total = 0;
+  if constexpr (KS::OVERLAY) {
+    /* survivors in chunks of W_NP_LANES lanes: narrowphase with its clip polygons in LDS, raw
+       contacts staged in LDS, then one lane per staged contact writes it at (prefix of its
+       survivor lane) + (its index), the order of the pass below -- no private (scratch) arrays */
+    static_assert(KS::BAIL && KS::MAXCON <= W_NP_STAGE, "compact narrowphase stage must hold MAXCON");
+    if (lane == 0) s.np_nstage = 0;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    for (int base = 0; base < nsurv; base += W_NP_LANES) {
+      const int slot = base + lane;
+      const bool act = lane < W_NP_LANES && slot < nsurv;
+      const int p = s.cand_off[act ? slot : 0];
+      int cnt = 0;
+      if (act) cnt = w_narrow_lds(m, s, p, lane);
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < W_NP_LANES; d <<= 1) {
+        const int y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+      }
+      const int off = total + incl - cnt;
+      total += rli(incl, W_NP_LANES - 1);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      const int nall = s.np_nstage;
+      const int nst = nall < W_NP_STAGE ? nall : W_NP_STAGE;
+      const int key = lane < nst ? s.np_key[lane] : 0;
+      const int src = key >> 3, kk = key & 7;
+      const int offs = shfi(off, src), ps = shfi(p, src);
+      if (lane < nst && offs + kk < KS::MAXCON) {
+        KRaw r;
+        r.pos[0] = s.np_stage[0][lane]; r.pos[1] = s.np_stage[1][lane]; r.pos[2] = s.np_stage[2][lane];
+        r.n[0] = s.np_stage[3][lane]; r.n[1] = s.np_stage[4][lane]; r.n[2] = s.np_stage[5][lane];
+        r.dist = s.np_stage[6][lane];
+        w_store_contact(m, s, offs + kk, ps, r);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (lane == 0) {
+        if (nall > W_NP_STAGE) s.ovf = 1; /* contacts were dropped from the stage: > MAXCON anyway */
+        s.np_nstage = 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (lane == 0) {
+      s.ncon = total < KS::MAXCON ? total : KS::MAXCON;
+      if (total > s.cap_con) s.ovf = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    return;
+  }
   for (int base = 0; base < nsurv; base += 64) {
     const int slot = base + lane;
     /* the box-box routine is inlined here: an out-of-line call from this divergent region was
