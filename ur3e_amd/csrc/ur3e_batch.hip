@@ -1075,6 +1075,22 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
 #ifndef W_COMPACT_WPE
 #define W_COMPACT_WPE 2
 #endif
+/* diagnostic build only (-DUR3E_WAVE_TRACE): per env of the last step launch, lane 0's
+   s_memrealtime (100 MHz) at start and end, XCC_ID:HW_ID, and did_reset | ncon << 8 | blockIdx << 32 */
+#ifdef UR3E_WAVE_TRACE
+#define UR3E_WAVE_TRACE_MAX 16384
+__device__ unsigned long long ur3e_wave_trace[UR3E_WAVE_TRACE_MAX][4];
+#endif
+
+/* XCD-aware env order: workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8), so workgroup
+   b runs env (b % 8) * (n / 8) + b / 8 -- each XCD steps one contiguous env range and neighbouring
+   envs, whose per-env scalars and state rows share cache lines, meet in the same L2 instead of
+   eight.  Envs are independent, so the order changes no result. */
+KD int k_xcd_env(int b, int n) {
+  if (n & 7) return b;
+  return (b & 7) * (n >> 3) + (b >> 3);
+}
+
 template <int NT, class KS>
 __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                   KConfig c, KState st, const double* __restrict__ actions, int adim,
@@ -1085,8 +1101,11 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
                                                   int* __restrict__ ovf_count) {
   __shared__ KS s;
   __shared__ WOut o;
-  const int e = blockIdx.x;
-  if (e >= st.n) return;
+  if ((int)blockIdx.x >= st.n) return;
+  const int e = k_xcd_env((int)blockIdx.x, st.n);
+#ifdef UR3E_WAVE_TRACE
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   WT_INIT();
   if (!w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o)) {
     if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = e;
@@ -1096,6 +1115,16 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
   w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
   WT(27);
   WT_FLUSH();
+#ifdef UR3E_WAVE_TRACE
+  if (threadIdx.x == 0 && e < UR3E_WAVE_TRACE_MAX) {
+    ur3e_wave_trace[e][0] = t_start;
+    ur3e_wave_trace[e][1] = __builtin_amdgcn_s_memrealtime();
+    ur3e_wave_trace[e][2] = ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                            (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4); /* XCC_ID : HW_ID */
+    ur3e_wave_trace[e][3] = (unsigned long long)o.did_reset | ((unsigned long long)s.ncon << 8) |
+                            ((unsigned long long)blockIdx.x << 32);
+  }
+#endif
 }
 
 /* full-capacity tier over the envs the compact tier queued (grid-stride over the list) */
@@ -1588,6 +1617,19 @@ extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long
 #else
   (void)cycles; (void)calls; (void)reset;
   return fail(UR3E_EINVAL, "library built without -DUR3E_STAGE_TIMING");
+#endif
+}
+
+/* diagnostic: copy the wave trace of the last step launch (UR3E_WAVE_TRACE builds only) */
+extern "C" int ur3e_debug_wave_trace(unsigned long long* out, int n) {
+#ifdef UR3E_WAVE_TRACE
+  if (!out || n < 0 || n > UR3E_WAVE_TRACE_MAX) return fail(UR3E_EINVAL, "bad wave-trace request");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(ur3e_wave_trace), sizeof(unsigned long long) * 4 * (size_t)n));
+  return UR3E_OK;
+#else
+  (void)out; (void)n;
+  return fail(UR3E_EINVAL, "library built without -DUR3E_WAVE_TRACE");
 #endif
 }
 
