@@ -92,6 +92,14 @@ def test_gym_v2_random_actions_short(epb):
     _run_pair("main", 0, 64, 60, _gym_actions, epb=epb)
 
 
+@pytest.mark.parametrize("n", [1, 13, 24])
+def test_gym_v2_env_counts(n):
+    """Env counts that are not / are multiples of the 8 XCDs: the step kernel's XCD-aware env order
+    is the identity for 1 and 13 envs and a real permutation for 24 (workgroup b -> env
+    (b % 8) * 3 + b / 8); every env must still match the oracle bit for bit."""
+    _run_pair("main", 0, n, 40, _gym_actions, seed=5)
+
+
 def _grasp_actions(rng, n, md):
     # actions concentrated around the mug with the gripper closing: exercises pad-box contacts
     a = np.zeros((n, 4))

@@ -1138,11 +1138,15 @@ __global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __rest
                                                        double* __restrict__ tobs_out,
                                                        const int* __restrict__ ovf_list,
                                                        const int* __restrict__ ovf_count,
+                                                       int* __restrict__ ovf_count_next,
                                                        unsigned long long* __restrict__ ovf_total) {
   __shared__ KSL s;
   __shared__ WOut o;
   const int cnt = *ovf_count;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *ovf_count_next = 0;
+    if (cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+  }
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int e = ovf_list[i];
     w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
@@ -1229,8 +1233,9 @@ struct ur3e_batch {
   int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
   int* d_ovf_list;
-  int* d_ovf_count;
+  int* d_ovf_count; /* [2], by step parity */
   unsigned long long* d_ovf_total;
+  unsigned int nstep; /* tiered steps launched (selects the overflow counter) */
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
@@ -1416,9 +1421,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
-  HIPCHK(hipMalloc(&b->d_ovf_count, sizeof(int)));
+  HIPCHK(hipMalloc(&b->d_ovf_count, 2 * sizeof(int))); /* [step parity]: see ur3e_batch_step */
   HIPCHK(hipMalloc(&b->d_ovf_total, sizeof(unsigned long long)));
-  HIPCHK(hipMemset(b->d_ovf_count, 0, sizeof(int)));
+  HIPCHK(hipMemset(b->d_ovf_count, 0, 2 * sizeof(int)));
   HIPCHK(hipMemset(b->d_ovf_total, 0, sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
@@ -1472,19 +1477,24 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
-    HIPCHK(hipMemsetAsync(b->d_ovf_count, 0, sizeof(int), st));
+    /* overflow counter double-buffered by step parity: this step's fallback kernel zeroes the
+       counter of the next step (the previous step's fallback kernel, its last reader, has finished
+       in stream order), so no memset launch per step */
+    int* cnt = b->d_ovf_count + (b->nstep & 1);
+    int* cnt_next = b->d_ovf_count + ((b->nstep + 1) & 1);
+    b->nstep++;
     if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
                          b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, b->d_ovf_count);
+                         b->d_ovf_list, cnt);
     else
       hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                          d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                         b->d_ovf_count);
+                         cnt);
     int grid = b->n < 512 ? b->n : 512;
     hipLaunchKernelGGL(w_env_step_list<128>, dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_count, b->d_ovf_total);
+                       cnt, cnt_next, b->d_ovf_total);
   } else if (b->wave_nt == 128)
     hipLaunchKernelGGL((w_env_step<128, KSL>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
