@@ -86,6 +86,8 @@ typedef struct ur3e_config_t {
   int tier_con_cap;      /* diagnostic (0 = off): the compact tier treats more than this many
                             contacts as overflow, to exercise the fallback path */
   double rot_joint_gains[12]; /* kp[6], kd[6] of the rotation PD in move_l (config_l.yml "rot") */
+  int np_chunk_lanes;    /* diagnostic (0 = 16): survivor lanes per compact-tier narrowphase chunk;
+                            smaller values exercise its multi-chunk path */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;

@@ -36,6 +36,7 @@ typedef struct {
   int envs_per_block;
   int tier_con_cap;
   double rot_joint_gains[12];
+  int np_chunk_lanes; /* GPU-tier diagnostic, unused here (layout mirror of ur3e_config_t) */
 } ur3o_config;
 
 /* the model has the sites the 24-d observation reads (main.xml) */

@@ -22,13 +22,14 @@ def _oracle_cfg(po, c):
 
 
 def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0, check_every=1, tier_con_cap=0,
-              task_gains=None, max_episode_steps=2500):
+              task_gains=None, max_episode_steps=2500, np_chunk_lanes=0):
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model(model_name)
     cfg = rt.make_config(task=task, frame_skip=frame_skip, model=md, seed=seed, envs_per_block=epb,
                          tier_con_cap=tier_con_cap, task_gains=task_gains, max_episode_steps=max_episode_steps,
+                         np_chunk_lanes=np_chunk_lanes,
                          reset_noise=(model_name == "main"),
                          reset_key=md["id_key_down"] if md["id_key_down"] >= 0 else -1)
     gb = rt.Batch(mc, cfg, n)
@@ -112,6 +113,15 @@ def _grasp_actions(rng, n, md):
 
 def test_gym_v2_grasp_region():
     _run_pair("main", 0, 64, 150, _grasp_actions, seed=3)
+
+
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_narrowphase_chunks(lanes):
+    """The compact tier's narrowphase runs survivor pairs in chunks of up to 16 lanes (clip
+    polygons and the contact stage live in LDS per chunk). With the diagnostic chunk width 1 or 3
+    every env with contacts goes through several chunks; contacts must still come out in
+    candidate order, bit-exact against the oracle."""
+    _run_pair("main", 0, 64, 100, _grasp_actions, seed=3, np_chunk_lanes=lanes)
 
 
 @pytest.mark.parametrize("cap", [2, 3])

@@ -392,6 +392,7 @@ struct KConfig {
   int env_id_offset;
   int epb;
   int tier_con_cap;
+  int np_lanes; /* survivor lanes per compact narrowphase chunk (1..W_NP_LANES) */
   int obs_sites; /* model has tcp / handle_site / ghost: the scripted tasks also emit the 24-d obs */
   KGains gains;
 };
@@ -830,6 +831,7 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
     s.nwarn = st.nwarn[e];
     s.ovf = 0;
     s.cap_con = (KS::BAIL && c.tier_con_cap > 0 && c.tier_con_cap < KS::MAXCON) ? c.tier_con_cap : KS::MAXCON;
+    if constexpr (KS::OVERLAY) s.np_lanes = c.np_lanes;
     o.t = st.t[e]; o.ep_len = st.ep_len[e]; o.ep_return = st.ep_return[e]; o.episode = st.episode[e];
     o.did_reset = 0; o.term = 0; o.trunc = 0; o.r = 0;
   }
@@ -1381,6 +1383,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.env_id_offset = cfg->env_id_offset;
   c.epb = cfg->envs_per_block > 0 && cfg->envs_per_block <= 64 ? cfg->envs_per_block : 16;
   c.tier_con_cap = cfg->tier_con_cap;
+  c.np_lanes = cfg->np_chunk_lanes > 0 && cfg->np_chunk_lanes < W_NP_LANES ? cfg->np_chunk_lanes : W_NP_LANES;
   c.obs_sites = model->id_site_tcp >= 0 && model->id_site_handle >= 0 && model->id_body_ghost >= 0;
   KPlan plan;
   build_plan(model, &plan);

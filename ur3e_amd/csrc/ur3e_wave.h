@@ -167,6 +167,7 @@ struct KSX<MC, ME, NVC, TREE, true> {
   double eq_p[UR3E_MAXEQ][6];  /* connect anchors p1, p2 in world coordinates */
   double site_vel[2][6];       /* [tcp, handle] mj_objectVelocity (world, [w, v]) */
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
+  int np_lanes; /* survivor lanes per narrowphase chunk (KConfig.np_lanes, <= W_NP_LANES) */
   unsigned long long tlast;
 #ifdef UR3E_STAGE_TIMING
   unsigned int tacc[32]; /* 32-bit: keeps the timing build's layout within 20 KB (with MAXCON 9) */
@@ -773,9 +774,10 @@ WD void r_collision(KModel m, KS& s) {
     if (lane == 0) s.np_nstage = 0;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    for (int base = 0; base < nsurv; base += W_NP_LANES) {
+    const int npl = s.np_lanes;
+    for (int base = 0; base < nsurv; base += npl) {
       const int slot = base + lane;
-      const bool act = lane < W_NP_LANES && slot < nsurv;
+      const bool act = lane < npl && slot < nsurv;
       const int p = s.cand_off[act ? slot : 0];
       int cnt = 0;
       if (act) cnt = w_narrow_lds(m, s, p, lane);
