@@ -355,3 +355,29 @@ def test_compact_kernel_occupancy():
     b.close()
     assert info["lds_bytes"] <= 20480, info
     assert info["envs_per_cu"] >= 8, info
+
+
+@pytest.mark.gpu
+def test_ppo_graph_update_matches_eager():
+    """Config C5 driver: the HIP-graph replay of the PPO minibatch update (three eager warm-up
+    minibatches, then capture) lands on the same policy as the eager update on the same rollout
+    (same seeds, same env): only Adam's device-side bias correction (capturable) rounds
+    differently, so parameters agree to 1e-5."""
+    torch = _torch()
+    from ur3e_amd.envs.vec_env import UR3eVecEnv
+    from ur3e_amd.envs.vec_normalize import VecNormalize
+    from ur3e_amd.rl.ppo import PPO
+    params, stats = [], []
+    for graphs in (False, True):
+        venv = UR3eVecEnv(num_envs=64, device=0, seed=0)
+        env = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10.0)
+        algo = PPO(env, n_steps=4, batch_size=32, n_epochs=2, device="cuda:0", seed=0, graphs=graphs)
+        algo.learn(1)
+        assert (algo._graphs is not None) == graphs
+        params.append(torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu())
+        stats.append(algo.stats)
+        venv.close()
+    d = (params[0] - params[1]).abs().max().item()
+    assert d < 1e-5, d
+    for k in stats[0]:
+        assert abs(stats[0][k] - stats[1][k]) < 1e-4 * max(1.0, abs(stats[0][k])), (k, stats)

@@ -91,7 +91,7 @@ class PPO:
     def __init__(self, env, n_steps: int = 16, batch_size: int = 256, n_epochs: int = 30, learning_rate: float = 3e-4,
                  gamma: float = 0.99, gae_lambda: float = 0.95, clip_range: float = 0.2, ent_coef: float = 0.01,
                  vf_coef: float = 0.5, max_grad_norm: float = 0.5, net_arch=(256, 256), device=None, seed: int = 0,
-                 group=None):
+                 group=None, graphs=None):
         self.env = env
         self.n_envs = env.num_envs
         self.device = torch.device(device) if device is not None else torch.device("cpu")
@@ -110,7 +110,20 @@ class PPO:
             import torch.distributed as dist
             for p in self.policy.parameters():
                 dist.broadcast(p.data, src=0, group=group)
-        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        # gradients live in ONE flat buffer (each parameter's .grad is a view of it): the multi-rank
+        # average is a single all-reduce on that buffer, with no flatten / unflatten copies
+        params = list(self.policy.parameters())
+        self._flat_grad = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=self.device)
+        off = 0
+        for p in params:
+            p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        # on the GPU the minibatch update is replayed from HIP graphs (a batch-256 update is a few
+        # hundred tiny kernels, launch-bound when issued one by one); Adam keeps its step count on
+        # the device for that (capturable)
+        self.use_graphs = (self.device.type == "cuda") if graphs is None else bool(graphs)
+        self.opt = torch.optim.Adam(params, lr=learning_rate, eps=1e-5, capturable=self.use_graphs)
+        self._graphs = None
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         T, N, f = n_steps, self.n_envs, dict(dtype=torch.float32, device=self.device)
@@ -177,45 +190,92 @@ class PPO:
     # -- update ----------------------------------------------------------------
     def _allreduce_grads(self):
         import torch.distributed as dist
-        params = [p for p in self.policy.parameters() if p.grad is not None]
-        flat = torch.cat([p.grad.reshape(-1) for p in params])
-        dist.all_reduce(flat, group=self.group)
-        flat /= dist.get_world_size(self.group)
-        off = 0
-        for p in params:
-            n = p.grad.numel()
-            p.grad.copy_(flat[off:off + n].view_as(p.grad))
-            off += n
+        dist.all_reduce(self._flat_grad, group=self.group)
+        self._flat_grad /= dist.get_world_size(self.group)
+
+    def _loss(self, idx):
+        """SB3 PPO.train minibatch loss (clipped surrogate, value MSE, entropy bonus)."""
+        v, logp, ent = self.policy.evaluate(self._obs_all[idx], self._act_all[idx])
+        adv = self._adv_s[idx]
+        if adv.numel() > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(logp - self._logp_all[idx])
+        pg = -torch.min(adv * ratio, adv * ratio.clamp(1 - self.clip, 1 + self.clip)).mean()
+        vf = torch.nn.functional.mse_loss(self._ret_s[idx], v)
+        ent_loss = -ent.mean()
+        return pg + self.ent_coef * ent_loss + self.vf_coef * vf, pg, vf, ent_loss
+
+    def _backward(self, idx):
+        self._flat_grad.zero_()
+        loss, pg, vf, ent_loss = self._loss(idx)
+        loss.backward()
+        return pg.detach(), vf.detach(), ent_loss.detach()
+
+    def _apply(self):
+        nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+        self.opt.step()
+
+    def _minibatch_eager(self, idx):
+        out = self._backward(idx)
+        if self.group is not None:
+            self._allreduce_grads()
+        self._apply()
+        return out
+
+    def _capture(self):
+        """Two graphs per minibatch: (zero grads, forward, backward) and (clip, Adam step); the
+        multi-rank gradient average runs between them as one eager RCCL all-reduce."""
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga):
+            self._g_out = self._backward(self._g_idx)
+        with torch.cuda.graph(gb, pool=ga.pool()):
+            self._apply()
+        self._graphs = (ga, gb)
+
+    def _minibatch_graph(self, idx):
+        self._g_idx.copy_(idx)
+        self._graphs[0].replay()
+        if self.group is not None:
+            self._allreduce_grads()
+        self._graphs[1].replay()
+        return self._g_out
 
     def train(self):
         T, N = self.n_steps, self.n_envs
-        obs = self.buf_obs.reshape(T * N, -1)
-        act = self.buf_act.reshape(T * N, -1)
-        old_logp, old_val = self.buf_logp.reshape(-1), self.buf_val.reshape(-1)
-        adv_all, ret_all = self.adv.reshape(-1), self.ret.reshape(-1)
+        B = self.batch_size
         total = T * N
-        last = {}
+        self._obs_all = self.buf_obs.reshape(total, -1)
+        self._act_all = self.buf_act.reshape(total, -1)
+        self._logp_all = self.buf_logp.reshape(-1)
+        if getattr(self, "_adv_s", None) is None:  # persistent: the graphs read these addresses
+            self._adv_s = torch.empty(total, dtype=torch.float32, device=self.device)
+            self._ret_s = torch.empty(total, dtype=torch.float32, device=self.device)
+            self._g_idx = torch.zeros(B, dtype=torch.long, device=self.device)
+        self._adv_s.copy_(self.adv.reshape(-1))
+        self._ret_s.copy_(self.ret.reshape(-1))
+        last = None
+        warm = 0
         for _ in range(self.n_epochs):
             perm = torch.randperm(total, generator=self.gen, device=self.device)
-            for s in range(0, total, self.batch_size):
-                idx = perm[s:s + self.batch_size]
-                v, logp, ent = self.policy.evaluate(obs[idx], act[idx])
-                adv = adv_all[idx]
-                if adv.numel() > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                ratio = torch.exp(logp - old_logp[idx])
-                pg = -torch.min(adv * ratio, adv * ratio.clamp(1 - self.clip, 1 + self.clip)).mean()
-                vf = torch.nn.functional.mse_loss(ret_all[idx], v)
-                ent_loss = -ent.mean()
-                loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
-                self.opt.zero_grad(set_to_none=False)
-                loss.backward()
-                if self.group is not None:
-                    self._allreduce_grads()
-                nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
-                self.opt.step()
-                last = {"policy_gradient_loss": pg.detach(), "value_loss": vf.detach(), "entropy_loss": ent_loss.detach()}
-        self.stats = {k: float(v) for k, v in last.items()}
+            for s in range(0, total, B):
+                idx = perm[s:s + B]
+                if not self.use_graphs or idx.numel() != B:
+                    last = self._minibatch_eager(idx)
+                elif self._graphs is None and warm < 3:
+                    # warm-up before capture (torch.cuda.graphs): real minibatch updates, run on a
+                    # side stream so that autograd and the BLAS handles settle outside the capture
+                    side = torch.cuda.Stream(device=self.device)
+                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(side):
+                        last = self._minibatch_eager(idx)
+                    torch.cuda.current_stream(self.device).wait_stream(side)
+                    warm += 1
+                else:
+                    if self._graphs is None:
+                        self._capture()
+                    last = self._minibatch_graph(idx)
+        if last is not None:
+            self.stats = dict(zip(("policy_gradient_loss", "value_loss", "entropy_loss"), (float(x) for x in last)))
 
     def learn(self, iterations: int = 1):
         """Returns per-iteration wall times {rollout_s, train_s}."""
