@@ -9,9 +9,9 @@ cd /tmp && export TMPDIR=/tmp
 cd $R
 timeout -k 10 300 python3 bench.py > $D/bench.json 2> $D/bench.err || exit $?
 tail -1 $D/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $D/trace.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-extra > $D/trace.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $D/pmc_$c -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $D/pmc_$c.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $D/pmc_$c -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $D/pmc_$c.log 2>&1 || exit $?
 done
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/pmc_sq -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $D/pmc_sq.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/pmc_sq -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $D/pmc_sq.log 2>&1 || exit $?
 find $D -name "*.csv" | head -20
