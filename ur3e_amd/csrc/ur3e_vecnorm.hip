@@ -28,9 +28,13 @@ int ur3e_internal_fail(int code, const char* msg);
 /* numpy pairwise_sum over a contiguous double array (numpy/_core/src/umath/loops_utils.h.src), of
    the values f(a[i]): blocks < 8 sum sequentially from 0.0, blocks <= 128 use 8 strided accumulators
    combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail, larger blocks split at
-   n/2 rounded down to a multiple of 8.  The recursion runs on an explicit stack. */
-template <class F>
-__device__ static double vn_pairwise(const double* a, int n, F f) {
+   n/2 rounded down to a multiple of 8.  The recursion runs on an explicit stack.  P is an LDS- or
+   global-address-space pointer: through a generic pointer every load of this serial chain would be
+   a FLAT load (LDS data at FLAT latency, and every wait counting both memory counters). */
+typedef const __attribute__((address_space(3))) double* VnLds;
+typedef const __attribute__((address_space(1))) double* VnGlobal;
+template <class P, class F>
+__device__ static double vn_pairwise(P a, int n, F f) {
   struct Fr { int off, len, stage; double left; };
   Fr stk[32];
   int sp = 0;
@@ -121,9 +125,16 @@ __global__ __launch_bounds__(VN_NT) void k_vn_stats(ur3e_vecnorm_stats_t st, int
     __threadfence_block();
     __syncthreads();
     if (tid == 0) {
-      const double* a = in_lds ? rbuf : st.returns;
-      const double bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
-      const double q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+      double bm, q;
+      if (in_lds) {
+        const VnLds a = (VnLds)rbuf;
+        bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
+        q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+      } else {
+        const VnGlobal a = (VnGlobal)st.returns;
+        bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
+        q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+      }
       const double c = *st.ret_count;
       vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);
       *st.ret_count = bn + c;
