@@ -35,6 +35,16 @@ ALGO_BYTES_PER_ENV_STEP = 1898
 FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
+def _profile_file(kind: str) -> str:
+    """profiles/<kind>_rNN.json of the latest round that has one (traffic: PMC HBM bytes per launch of
+    the step kernel; flops: the oracle-counted FP64 flops per env-step)"""
+    for r in ("r02", "r01"):
+        p = os.path.join(REPO, "profiles", f"{kind}_{r}.json")
+        if os.path.exists(p):
+            return p
+    return os.path.join(REPO, "profiles", f"{kind}_r01.json")
+
+
 def _state_diff(gb, ob):
     """max |qpos - ref|, max |qvel - ref| and contact-count mismatches, GPU handle vs oracle batch"""
     qp, qv, _ = gb.get_state()
@@ -45,21 +55,49 @@ def _state_diff(gb, ob):
                 ncon_mismatch_envs=int((ncon != onc).sum()))
 
 
-def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0):
-    """The cpu_baseline leg.  (1) Time the CPU oracle (oracle/, OpenMP over envs) on a bounded sample of
-    the bench workload: n_envs_sample gym ur3e-v2 envs x `steps` env-steps.  (2) As the checker, replay
-    the same seeded actions through a fresh GPU handle and report the metric's second half,
-    max |qpos - ref| after `steps` env-steps (the oracle is the reference here: MuJoCo is absent)."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _host_threads() -> int:
+    """The CPU share of this process: OMP_NUM_THREADS when set (16 per GPU on the box), else the
+    affinity mask (os.cpu_count() reports the whole machine there)."""
+    if os.environ.get("OMP_NUM_THREADS"):
+        return int(os.environ["OMP_NUM_THREADS"])
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_core_steps=400):
+    """The cpu_baseline leg.  The oracle (oracle/, the same algorithm in C) is compiled for this host
+    (-O3 -march=native -ffp-contract=off, OpenMP over envs) and timed on a bounded sample of the bench
+    workload: (1) all host threads: n_envs_sample gym ur3e-v2 envs x `steps` env-steps; (2) one thread:
+    one_core_envs x one_core_steps.  As the checker, the same seeded actions are replayed through a
+    fresh GPU handle, giving the metric's second half, max |qpos - ref| after `steps` env-steps (the
+    oracle is the reference here: MuJoCo is absent)."""
+    import tempfile
+
     import torch
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
+    L = po.load_native(os.path.join(tempfile.gettempdir(), f"ur3e_oracle_native_{os.getpid()}"))
+    threads = _host_threads()
     md, mc = rt.load_model("main")
     c = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=seed)
-    ob = po.OracleBatch(mc, po.config_from(c), n_envs_sample)
-    gb = rt.Batch(mc, c, n_envs_sample)
-    rng = np.random.default_rng(seed)
     lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
     hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
+    # (1) all threads, with the GPU replaying the same actions for the parity figure
+    L.ur3o_set_threads(threads)
+    ob = po.OracleBatch(mc, po.config_from(c), n_envs_sample, L=L)
+    gb = rt.Batch(mc, c, n_envs_sample)
+    rng = np.random.default_rng(seed)
     dt = 0.0
     for _ in range(steps):
         a = rng.uniform(lo, hi, size=(n_envs_sample, 4))
@@ -71,10 +109,25 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0):
     parity = dict(workload="gym ur3e-v2, uniform random actions", envs=n_envs_sample, steps=steps,
                   **_state_diff(gb, ob))
     gb.close()
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    base = dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=cores, kind="port",
-                sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps), "
-                       f"oracle/ C restatement, OpenMP {cores} threads, {dt:.1f} s")
+    # (2) one thread
+    L.ur3o_set_threads(1)
+    ob1 = po.OracleBatch(mc, po.config_from(c), one_core_envs, L=L)
+    rng = np.random.default_rng(seed + 1)
+    dt1 = 0.0
+    for _ in range(one_core_steps):
+        a = rng.uniform(lo, hi, size=(one_core_envs, 4))
+        t0 = time.perf_counter()
+        ob1.step(a)
+        dt1 += time.perf_counter() - t0
+    L.ur3o_set_threads(threads)
+    cpu = _cpu_model()
+    build = "gcc -O3 -march=native -ffp-contract=off -fopenmp (compiled on this host)"
+    base = dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=threads, kind="port",
+                sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps) from reset, "
+                       f"oracle/ C restatement, OpenMP {threads} threads, {dt:.1f} s",
+                cpu_model=cpu, build=build,
+                one_core={"value": one_core_envs * one_core_steps / dt1, "unit": "env-steps/s", "cores": 1,
+                          "sample": f"{one_core_envs} envs x {one_core_steps} env-steps, 1 thread, {dt1:.1f} s"})
     return base, parity
 
 
@@ -119,11 +172,27 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
     out["C2_ur3e_2f85_move_j"] = {"value": timed(lambda: b.step(next(it))), "unit": "env-steps/s",
                                   "envs": n_envs, "substeps_per_env_step": 1}
     b.close()
+    # C3 is timed over the grasp: rows 1500-2600 of build_traj_l_pick_place (build_traj.py:28-59: the
+    # descent to the mug ends at row 1800, the gripper closes and the lift starts), reached untimed
     drv = MoveLMug(n_envs, reset_mode="low", seed=0)
-    rows = [drv.traj.row(t) for t in range(warmup + steps)]
+    g0, g1 = 1500, 2600
+    for t in range(g0):
+        drv.batch.step(drv.traj.row(t))
+    rows = [drv.traj.row(t) for t in range(g0, g1)]
+    ovf0 = drv.batch.overflow_count()
     it = iter(rows)
-    out["C3_main_move_l_mug"] = {"value": timed(lambda: drv.batch.step(next(it))), "unit": "env-steps/s",
-                                 "envs": n_envs, "substeps_per_env_step": 1}
+    steps_c3 = g1 - g0
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps_c3):
+        drv.batch.step(next(it))
+    e1.record()
+    torch.cuda.synchronize()
+    fb = drv.batch.overflow_count() - ovf0
+    out["C3_main_move_l_mug"] = {"value": n_envs * steps_c3 / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s",
+                                 "envs": n_envs, "substeps_per_env_step": 1, "rows": [g0, g1],
+                                 "fallback_env_steps_frac": fb / float(n_envs * steps_c3)}
     drv.close()
     return out
 
@@ -160,6 +229,8 @@ def main():
     ap.add_argument("--cpu-sample-steps", type=int, default=1000)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C3 secondary throughput numbers")
+    ap.add_argument("--pre-steps", type=int, default=500,
+                    help="untimed env-steps after reset, so the timed window is mid-episode (contact regime)")
     ap.add_argument("--gather-self", action="store_true",
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
     args = ap.parse_args()
@@ -215,15 +286,14 @@ def main():
         nstep = [0]
 
     step_events = []
-    # synthetic inputs are generated before the timed region and stay resident in HBM (one
-    # [n, 4] action batch per step); the timed loop runs only the env step (and the gather)
-    acts = lo + (hi - lo) * torch.rand((args.warmup + args.steps, n, 4), dtype=torch.float64, device=dev,
-                                       generator=gen)
-    nact = [0]
+    # synthetic inputs are generated before the timed regions and stay resident in HBM (one [n, 4]
+    # action batch per step); the timed loops run only the env step (and the gather)
+    n_fresh = min(args.steps, args.pre_steps)
 
-    def one_step(timed=False):
-        a = acts[nact[0]]
-        nact[0] += 1
+    def draw(k):
+        return lo + (hi - lo) * torch.rand((k, n, 4), dtype=torch.float64, device=dev, generator=gen)
+
+    def one_step(a, timed=False):
         if timed:  # HIP events on the stream the library launches on (torch's current stream)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -245,8 +315,23 @@ def main():
             with torch.cuda.stream(comm):
                 dist.gather(payload, glists[k], dst=0)
 
-    for _ in range(args.warmup):
-        one_step()
+    # (1) fresh-reset window (secondary figure): the first n_fresh env-steps after reset, timed on the
+    # stream; (2) the rest of the --pre-steps, untimed, so the headline window is mid-episode
+    acts_fresh = draw(n_fresh)
+    torch.cuda.synchronize()
+    fe0, fe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fe0.record()
+    for i in range(n_fresh):
+        one_step(acts_fresh[i])
+    fe1.record()
+    for _ in range(args.pre_steps - n_fresh):
+        one_step(draw(1)[0])
+    torch.cuda.synchronize()
+    fresh_ms = fe0.elapsed_time(fe1) / max(n_fresh, 1)
+    del acts_fresh
+    acts = draw(args.warmup + args.steps)
+    for i in range(args.warmup):
+        one_step(acts[i])
     ovf0 = batch.overflow_count()
     torch.cuda.synchronize()
     if world > 1:
@@ -257,7 +342,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
-        one_step(timed=True)
+        one_step(acts[args.warmup + i], timed=True)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -281,7 +366,7 @@ def main():
     if rank == 0:
         achieved = ALGO_BYTES_PER_ENV_STEP * n / (step_kernel_ms * 1e-3) / 1e9
         prof_traffic = None
-        tf = os.path.join(REPO, "profiles", "traffic_r01.json")
+        tf = _profile_file("traffic")
         if os.path.exists(tf):
             try:
                 with open(tf) as f:
@@ -289,7 +374,7 @@ def main():
             except Exception:
                 prof_traffic = None
         fp64 = None
-        ff = os.path.join(REPO, "profiles", "flops_r01.json")
+        ff = _profile_file("flops")
         if os.path.exists(ff):
             try:
                 with open(ff) as f:
@@ -297,7 +382,7 @@ def main():
                 ach = fpe * n / (step_kernel_ms * 1e-3) / 1e12
                 fp64 = {"bound": "fp64-vector", "achieved": ach, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": ach / FP64_VECTOR_PEAK_TFLOPS, "flops_per_env_step": fpe,
-                        "source": "profiles/flops_r01.json (tools/count_flops.py: counting build of the oracle)"}
+                        "source": os.path.relpath(ff, REPO) + " (tools/count_flops.py: counting build of the oracle)"}
             except Exception:
                 fp64 = None
         cpu, parity = None, None
@@ -327,7 +412,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (uniform random actions in the ur3e-v2 action Box, generated into HBM before the timed region; stochastic 'high' mug resets)",
+            "data": "synthetic (uniform random actions in the ur3e-v2 action Box, generated into HBM before the timed region; stochastic 'high' mug resets; timed window starts after --pre-steps untimed env-steps, mid-episode)",
             "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
                        "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (20 KB lifetime-overlaid LDS working set, 256 VGPRs: 8 envs/CU, 2 per SIMD)"
@@ -337,6 +422,12 @@ def main():
                        "kernel_resources": batch_kinfo,
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
+            "window": {"pre_steps_untimed": args.pre_steps,
+                       "timed_env_steps_since_reset": [args.pre_steps + args.warmup,
+                                                       args.pre_steps + args.warmup + args.steps],
+                       "fresh_reset": {"value": n * world / (fresh_ms * 1e-3), "unit": "env-steps/s",
+                                       "env_steps_since_reset": [0, n_fresh],
+                                       "note": "rank-0 stream time of the first env-steps after reset"}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic,
                          "kernel": "w_env_step<64,KSS_NV> (+ w_env_step_list<128> fallback)",

@@ -9,6 +9,12 @@
  * on success, a negative UR3E_E* code otherwise; ur3e_last_error() gives a
  * thread-local message.  A handle is not thread-safe.
  *
+ * Graph capture: ur3e_batch_step, _reset, _set_state and the getters keep all of their control
+ * state on the device (the overflow list of the two-tier step is reset by its own fallback kernel),
+ * so a sequence of them can be captured into a HIP graph (hipStreamBeginCapture, or
+ * torch.cuda.graph) and replayed any number of times.  ur3e_batch_overflow_count and
+ * ur3e_batch_last_step_ms synchronise and must not be captured.
+ *
  * Reference interfaces each entry point replaces (the reference's boundary is
  * Python — gymnasium Env + MuJoCo C API):
  *
@@ -152,7 +158,9 @@ int ur3e_batch_nu(const ur3e_batch_t* b);
    workgroup, registers per lane */
 int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs);
 
-/* profiling: events recorded around the most recent step kernel on its stream */
+/* profiling: with timing on (off by default), every ur3e_batch_step that is not being captured into
+   a graph records a pair of HIP events around its kernels; last_step_ms reads the most recent pair */
+int ur3e_batch_set_timing(ur3e_batch_t* b, int on);
 int ur3e_batch_last_step_ms(ur3e_batch_t* b, float* ms);
 
 #ifdef __cplusplus

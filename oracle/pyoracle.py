@@ -31,6 +31,27 @@ def lib():
     return _lib
 
 
+_SRCS = ("ur3e_oracle.c", "ur3e_oracle_batch.c")
+
+
+def build_native(out_dir: str) -> str:
+    """Compile the oracle for THIS host's CPU (-O3 -march=native, contraction still off, so results
+    are unchanged) into out_dir and return the .so path.  Used by bench.py's cpu_baseline leg on the
+    GPU box, where the host CPU differs from the build container's."""
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "libur3e_oracle_native.so")
+    cc = os.environ.get("CC", "gcc")
+    cmd = [cc, "-O3", "-march=native", "-fPIC", "-std=c99", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
+           "-shared", "-o", so] + [os.path.join(_HERE, f) for f in _SRCS] + ["-lm"]
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return so
+
+
+def load_native(out_dir: str):
+    L = ctypes.CDLL(build_native(out_dir))
+    return L
+
+
 class OracleConfig(ctypes.Structure):
     _fields_ = [
         ("task", ctypes.c_int), ("frame_skip", ctypes.c_int), ("max_episode_steps", ctypes.c_int),

@@ -21,6 +21,18 @@
 #include <string.h>
 
 #include "ur3e_oracle.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* OpenMP threads of the batch calls (bench.py's cpu_baseline times 1 thread and all threads) */
+void ur3o_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
 
 typedef struct {
   int task;

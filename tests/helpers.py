@@ -24,6 +24,8 @@ class OracleStepper:
         self.ob = po.OracleBatch(mc, oracle_config(po, cfg), n)
         self.n = n
         self.obs = torch.from_numpy(self.ob.obs.copy())
+        self.obs_dim = s["obs_dim"]
+        self.act_dim = len(s["low"])
 
     def reset(self):
         return self.torch.from_numpy(self.ob.obs.copy())

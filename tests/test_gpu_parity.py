@@ -306,8 +306,8 @@ def test_collect_demos_batched(mode):
     col.close()
 
 
-@pytest.mark.parametrize("norm_reward", [False, True])
-def test_vecnormalize_gpu_matches_sb3(norm_reward):
+@pytest.mark.parametrize("norm_reward,n", [(False, 1000), (True, 1000), (True, 20000)])
+def test_vecnormalize_gpu_matches_sb3(norm_reward, n):
     """On-device VecNormalize (train_rl.py:57) vs the numpy restatement of SB3 2.7.0 on the same raw
     step outputs: running obs/return statistics, normalised f32 obs, rewards and terminal obs are
     bit-identical (numpy's axis-0 sequential and 1-D pairwise reduction orders)."""
@@ -315,7 +315,8 @@ def test_vecnormalize_gpu_matches_sb3(norm_reward):
     from oracle.vecnorm_ref import VecNormalizeRef
     from ur3e_amd.envs.vec_env import UR3eVecEnv
     from ur3e_amd.envs.vec_normalize import VecNormalize
-    n = 1000  # not a multiple of 8 or 128: exercises every branch of the pairwise sum
+    # n = 1000 is not a multiple of 8 or 128: every branch of the pairwise sum; n = 20000 spans three
+    # of numpy's 8192-element reduction buffers (the returns' sums are blocked like numpy's)
     venv = UR3eVecEnv(num_envs=n, seed=4, max_episode_steps=7)
     vn = VecNormalize(venv, norm_reward=norm_reward, clip_obs=10.0)
     ref = VecNormalizeRef(n, 24, norm_reward=norm_reward, clip_obs=10.0)

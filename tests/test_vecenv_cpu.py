@@ -76,3 +76,20 @@ def test_register_ids_match_reference():
     for entry in register_envs.IDS.values():
         cls = register_envs._resolve(entry)
         assert cls.metadata["render_fps"] == 500
+
+
+def test_vecenv_attr_methods():
+    """SB3 VecEnv attribute API on the batched env: set_attr honours indices, get_attr returns
+    per-env values, env_method answers render and refuses unknown methods."""
+    n = 4
+    env = UR3eVecEnv(num_envs=n, stepper=OracleStepper(n, seed=3, max_episode_steps=5))
+    assert env.get_attr("render_mode") == [None] * n
+    env.set_attr("tag", 7, indices=[1, 3])
+    assert env.get_attr("tag") == [None, 7, None, 7]
+    assert env.get_attr("tag", indices=1) == [7]
+    assert env.env_method("render", indices=[0, 2]) == [None, None]
+    with pytest.raises(AttributeError):
+        env.env_method("no_such_method")
+    with pytest.raises(AttributeError):
+        env.get_attr("no_such_attr")
+    env.close()

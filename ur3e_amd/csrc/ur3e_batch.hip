@@ -1116,7 +1116,12 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
 #endif
   WT_INIT();
   if (!w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o)) {
-    if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = e;
+    if (threadIdx.x == 0) {
+      /* each env is appended at most once per step and the fallback kernel re-zeroes the counter,
+         so the slot is < n; the bound check keeps a corrupted counter from writing out of range */
+      const int slot = atomicAdd(ovf_count, 1);
+      if (slot < st.n) ovf_list[slot] = e;
+    }
     WT_FLUSH();
     return;
   }
@@ -1135,7 +1140,11 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
 #endif
 }
 
-/* full-capacity tier over the envs the compact tier queued (grid-stride over the list) */
+/* full-capacity tier over the envs the compact tier queued (grid-stride over the list).
+   ovf_ctl = {count, blocks_done}: every workgroup reads the count, then the last workgroup to have
+   read it re-zeroes both, so the next step's compact kernel starts from an empty list.  The counter
+   lives and is reset entirely on the device, so a step captured into a HIP graph replays correctly
+   any number of times (no host-side step parity baked into the graph). */
 template <int NT>
 __global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __restrict__ m,
                                                        const KPlan* __restrict__ pl, KConfig c, KState st,
@@ -1144,17 +1153,23 @@ __global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __rest
                                                        unsigned char* __restrict__ term_out,
                                                        unsigned char* __restrict__ trunc_out,
                                                        double* __restrict__ tobs_out,
-                                                       const int* __restrict__ ovf_list,
-                                                       const int* __restrict__ ovf_count,
-                                                       int* __restrict__ ovf_count_next,
+                                                       const int* __restrict__ ovf_list, int* ovf_ctl,
                                                        unsigned long long* __restrict__ ovf_total) {
   __shared__ KSL s;
   __shared__ WOut o;
-  const int cnt = *ovf_count;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *ovf_count_next = 0;
-    if (cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+  __shared__ int s_cnt;
+  if (threadIdx.x == 0) {
+    int cnt = __hip_atomic_load(ovf_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cnt = cnt < st.n ? cnt : st.n;
+    s_cnt = cnt;
+    if (atomicAdd(ovf_ctl + 1, 1) == (int)gridDim.x - 1) { /* every workgroup has read the count */
+      atomicExch(ovf_ctl, 0);
+      atomicExch(ovf_ctl + 1, 0);
+      if (cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+    }
   }
+  SYNC();
+  const int cnt = s_cnt;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int e = ovf_list[i];
     w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
@@ -1241,15 +1256,15 @@ struct ur3e_batch {
   int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
   int* d_ovf_list;
-  int* d_ovf_count; /* [2], by step parity */
+  int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
   unsigned long long* d_ovf_total;
-  unsigned int nstep; /* tiered steps launched (selects the overflow counter) */
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
   KConfig cfg;
   KState st;
   hipEvent_t ev0, ev1;
+  int timing; /* record ev0/ev1 around each step (ur3e_batch_set_timing); off by default */
   int timed;
 };
 
@@ -1378,6 +1393,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->tiered = tiered;
   b->host_model = *model;
   b->timed = 0;
+  b->timing = 0;
   KConfig& c = b->cfg;
   c.task = cfg->task;
   c.frame_skip = cfg->frame_skip > 0 ? cfg->frame_skip : 1;
@@ -1430,9 +1446,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
-  HIPCHK(hipMalloc(&b->d_ovf_count, 2 * sizeof(int))); /* [step parity]: see ur3e_batch_step */
+  HIPCHK(hipMalloc(&b->d_ovf_ctl, 2 * sizeof(int)));
   HIPCHK(hipMalloc(&b->d_ovf_total, sizeof(unsigned long long)));
-  HIPCHK(hipMemset(b->d_ovf_count, 0, 2 * sizeof(int)));
+  HIPCHK(hipMemset(b->d_ovf_ctl, 0, 2 * sizeof(int)));
   HIPCHK(hipMemset(b->d_ovf_total, 0, sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
@@ -1448,7 +1464,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
   void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
-                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->d_ovf_list, b->d_ovf_count,
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->d_ovf_list, b->d_ovf_ctl,
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   (void)hipEventDestroy(b->ev0);
@@ -1484,40 +1500,50 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   if (adim != need) return fail(UR3E_EINVAL, "action dimension mismatch for task (expected " + std::to_string(need) + ")");
   HIPCHK(hipSetDevice(b->device));
   hipStream_t st = (hipStream_t)stream;
-  HIPCHK(hipEventRecord(b->ev0, st));
+  /* the step only enqueues kernels whose control state is on the device, so it may be captured into
+     a HIP graph; profiling events are recorded only when requested and never during a capture */
+  int record = b->timing;
+  if (record) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cs));
+    record = cs == hipStreamCaptureStatusNone;
+  }
+  if (record) HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
-    /* overflow counter double-buffered by step parity: this step's fallback kernel zeroes the
-       counter of the next step (the previous step's fallback kernel, its last reader, has finished
-       in stream order), so no memset launch per step */
-    int* cnt = b->d_ovf_count + (b->nstep & 1);
-    int* cnt_next = b->d_ovf_count + ((b->nstep + 1) & 1);
-    b->nstep++;
     if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
                          b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, cnt);
+                         b->d_ovf_list, b->d_ovf_ctl);
     else
       hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                          d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                         cnt);
+                         b->d_ovf_ctl);
     int grid = b->n < 512 ? b->n : 512;
     hipLaunchKernelGGL(w_env_step_list<128>, dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       cnt, cnt_next, b->d_ovf_total);
+                       b->d_ovf_ctl, b->d_ovf_total);
   } else if (b->wave_nt == 128)
     hipLaunchKernelGGL((w_env_step<128, KSL>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_count);
+                       b->d_ovf_ctl);
   else if (b->wave_nt == 64)
     hipLaunchKernelGGL((w_env_step<64, KSL>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_count);
+                       b->d_ovf_ctl);
   else
     hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
                        d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(b->ev1, st));
-  b->timed = 1;
+  if (record) {
+    HIPCHK(hipEventRecord(b->ev1, st));
+    b->timed = 1;
+  }
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_set_timing(ur3e_batch_t* b, int on) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  b->timing = on != 0;
   return UR3E_OK;
 }
 
@@ -1669,7 +1695,7 @@ extern "C" int ur3e_batch_nu(const ur3e_batch_t* b) { return b ? b->host_model.n
 
 extern "C" int ur3e_batch_last_step_ms(ur3e_batch_t* b, float* ms) {
   if (!b || !ms) return fail(UR3E_EINVAL, "null argument");
-  if (!b->timed) return fail(UR3E_EINVAL, "no step recorded");
+  if (!b->timed) return fail(UR3E_EINVAL, "no step recorded (enable with ur3e_batch_set_timing)");
   HIPCHK(hipEventSynchronize(b->ev1));
   HIPCHK(hipEventElapsedTime(ms, b->ev0, b->ev1));
   return UR3E_OK;

@@ -3,8 +3,8 @@
  *
  * k_vn_stats (two workgroups of 1024 threads on two CUs, rows staged through LDS):
  *   block 1: returns = returns * gamma + reward (all threads), then thread 0 runs numpy's pairwise
- *     summation (8 accumulators per <=128 block, halves rounded down to multiples of 8) for the
- *     1-D mean and var of the returns;
+ *     summation (8 accumulators per <=128 block, halves rounded down to multiples of 8) over each
+ *     8192-element buffer, the buffer sums added in order, for the 1-D mean and var of the returns;
  *   block 0, thread j < dim: column j of obs [n, dim]: mean = (((x0 + x1) + x2) + ...) / n and
  *     var = sum((x - mean)^2) / n in the same row-sequential order numpy uses for an axis-0
  *     reduction of a C-contiguous array, then RunningMeanStd.update_from_moments.
@@ -81,6 +81,18 @@ __device__ static double vn_pairwise(P a, int n, F f) {
   }
 }
 
+/* a 1-D np.sum / np.mean of a contiguous double array: numpy's reduction iterator hands the add loop
+   buffers of at most NPY_BUFSIZE = 8192 elements and accumulates the per-buffer pairwise sums in
+   order, starting from the additive identity -- for n > 8192 a single whole-array pairwise sum would
+   round differently */
+#define VN_NP_BUFSIZE 8192
+template <class P, class F>
+__device__ static double vn_sum(P a, int n, F f) {
+  double res = 0.0;
+  for (int b = 0; b < n; b += VN_NP_BUFSIZE) res = res + vn_pairwise(a + b, n - b < VN_NP_BUFSIZE ? n - b : VN_NP_BUFSIZE, f);
+  return res;
+}
+
 /* RunningMeanStd.update_from_moments in the operation order of common/running_mean_std.py; the
    caller stores the new count (shared by all columns) once */
 __device__ static void vn_moments(double* mean, double* var, double c, double bmean, double bvar, double bcount) {
@@ -128,12 +140,12 @@ __global__ __launch_bounds__(VN_NT) void k_vn_stats(ur3e_vecnorm_stats_t st, int
       double bm, q;
       if (in_lds) {
         const VnLds a = (VnLds)rbuf;
-        bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
-        q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+        bm = vn_sum(a, n, [](double x) { return x; }) / bn;
+        q = vn_sum(a, n, [bm](double x) { const double d = x - bm; return d * d; });
       } else {
         const VnGlobal a = (VnGlobal)st.returns;
-        bm = vn_pairwise(a, n, [](double x) { return x; }) / bn;
-        q = vn_pairwise(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+        bm = vn_sum(a, n, [](double x) { return x; }) / bn;
+        q = vn_sum(a, n, [bm](double x) { const double d = x - bm; return d * d; });
       }
       const double c = *st.ret_count;
       vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);

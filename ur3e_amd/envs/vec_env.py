@@ -27,10 +27,24 @@ except Exception:  # pragma: no cover
     _SB3VecEnv = object
 
 
+def _default_stepper(env_id: str, num_envs: int, device: int, seed: int, env_id_offset: int, envs_per_block: int,
+                     max_episode_steps: int | None):
+    """The product stepper: num_envs envs of `env_id` resident on GPU `device` (runtime.Batch)."""
+    from .. import runtime as rt
+    s = spec(env_id)
+    md, mc = rt.load_model("main")
+    T = s["T"] if max_episode_steps is None else max_episode_steps
+    cfg = rt.make_config(task=s["task"], frame_skip=s["frame_skip"], max_episode_steps=T, model=md, seed=seed,
+                         env_id_offset=env_id_offset, envs_per_block=envs_per_block, task_gains=s["gains"])
+    return rt.Batch(mc, cfg, num_envs, device=device)
+
+
 class UR3eVecEnv(_SB3VecEnv):
     def __init__(self, num_envs: int = 4096, device: int = 0, seed: int = 0, stepper=None, env_id_offset: int = 0,
                  envs_per_block: int = 0, max_episode_steps: int | None = None,
-                 env_id: str = "gymnasium_env/ur3e-v2"):
+                 env_id: str = "gymnasium_env/ur3e-v2", render_mode=None):
+        """`render_mode` is accepted for env_kwargs compatibility (train_rl.py:41 passes "human" when
+        config_rl.yml:14 visualize is True) and ignored: rendering is out of scope."""
         s = spec(env_id)
         self.env_id = env_id
         self.num_envs = num_envs
@@ -38,13 +52,13 @@ class UR3eVecEnv(_SB3VecEnv):
         self.action_space = Box(low=s["low"], high=s["high"], dtype=np.float64)
         self.render_mode = None
         if stepper is None:
-            from .. import runtime as rt
-            md, mc = rt.load_model("main")
-            T = s["T"] if max_episode_steps is None else max_episode_steps
-            cfg = rt.make_config(task=s["task"], frame_skip=s["frame_skip"], max_episode_steps=T,
-                                 model=md, seed=seed, env_id_offset=env_id_offset, envs_per_block=envs_per_block,
-                                 task_gains=s["gains"])
-            stepper = rt.Batch(mc, cfg, num_envs, device=device)
+            stepper = _default_stepper(env_id, num_envs, device, seed, env_id_offset, envs_per_block,
+                                       max_episode_steps)
+        if _SB3VecEnv is not object:  # pragma: no cover - SB3 is not installed in this image
+            try:  # SB3 2.x: num_envs, spaces, reset_infos, _seeds/_options, render_mode, metadata
+                _SB3VecEnv.__init__(self, num_envs, self.observation_space, self.action_space)
+            except TypeError:
+                pass
         self.stepper = stepper
         self._actions = None
         self._ep_ret = np.zeros(num_envs)
@@ -106,14 +120,35 @@ class UR3eVecEnv(_SB3VecEnv):
         return [seed] * self.num_envs
 
     def get_attr(self, attr_name, indices=None):
-        n = len(self._indices(indices))
-        return [self._attrs.get(attr_name, getattr(self, attr_name, None))] * n
+        """Per-env attribute values: values stored by set_attr for that env, else the (shared) attribute
+        of the batched env.  Raises AttributeError like SB3 for a name that exists nowhere."""
+        idx = self._indices(indices)
+        per_env = self._attrs.get(attr_name)
+        if per_env is None:
+            if attr_name == "render_mode":
+                return [self.render_mode] * len(idx)
+            val = getattr(self, attr_name)
+            return [val] * len(idx)
+        return [per_env[i] for i in idx]
 
     def set_attr(self, attr_name, value, indices=None):
-        self._attrs[attr_name] = value
+        """Store `value` for the selected envs only (SB3 semantics: one value, broadcast to `indices`)."""
+        if attr_name not in self._attrs:
+            cur = getattr(self, attr_name, None)
+            self._attrs[attr_name] = [cur] * self.num_envs
+        for i in self._indices(indices):
+            self._attrs[attr_name][i] = value
 
-    def env_method(self, method_name, *args, indices=None, **kwargs):
-        return [None] * len(self._indices(indices))
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        """Call a method of the per-env gymnasium facade for the selected envs.  Only the methods a
+        batched env can answer per env exist: render (None: rendering is out of scope) and the
+        attribute getters; anything else raises AttributeError instead of silently returning None."""
+        idx = self._indices(indices)
+        if method_name == "render":
+            return [None] * len(idx)
+        if method_name in ("get_wrapper_attr", "__getattribute__"):
+            return [v for v in self.get_attr(method_args[0], idx)]
+        raise AttributeError(f"UR3eVecEnv: env_method({method_name!r}) has no per-env meaning on the batched env")
 
     def env_is_wrapped(self, wrapper_class, indices=None):
         return [False] * len(self._indices(indices))
@@ -126,7 +161,7 @@ class UR3eVecEnv(_SB3VecEnv):
             return range(self.num_envs)
         if isinstance(indices, int):
             return [indices]
-        return indices
+        return list(indices)
 
 
 def _np(x):

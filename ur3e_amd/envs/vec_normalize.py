@@ -195,6 +195,13 @@ class VecNormalize:
 
     @classmethod
     def load(cls, path, venv):
+        """Load statistics written by save() (.npz).  SB3's VecNormalize.load reads a pickle of the whole
+        wrapper (train_rl.py's resume branch); pickles are never loaded here (they execute code), so an
+        SB3 file is refused with a clear message instead of failing inside np.load."""
+        import zipfile
+        if not zipfile.is_zipfile(path):
+            raise ValueError(f"{path!r} is not a VecNormalize .npz written by ur3e_amd (SB3 pickles are not "
+                             "loaded: re-save the statistics with VecNormalize.save from this package)")
         z = np.load(path)  # allow_pickle=False
         c = z["cfg"]
         self = cls(venv, training=bool(c[0]), norm_obs=bool(c[1]), norm_reward=bool(c[2]), clip_obs=float(c[3]),

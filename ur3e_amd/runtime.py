@@ -70,6 +70,7 @@ def load_library():
     L.ur3e_batch_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.ur3e_batch_get_info.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ur3e_batch_last_step_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.ur3e_batch_set_timing.argtypes = [vp, ip]
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
@@ -125,6 +126,15 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     return c
 
 
+def action_dim(task: int, nu: int) -> int:
+    """Width of one env's action row for a task (what ur3e_batch_step checks `adim` against)."""
+    if task in (TASK_GYM_V2, TASK_GYM_V0, TASK_IMIT_INDIRECT):
+        return 4
+    if task in (TASK_CTRL, TASK_IMIT_DIRECT):
+        return nu
+    return 7
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -149,6 +159,7 @@ class Batch:
         self.h = h
         f64 = dict(dtype=torch.float64, device=self.device)
         self.obs_dim = self.L.ur3e_batch_obs_dim(h)
+        self.act_dim = action_dim(cfg.task, self.nu)
         self.obs = torch.zeros((n_envs, self.obs_dim), **f64)
         self.reward = torch.zeros(n_envs, **f64)
         self.terminated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
@@ -247,12 +258,16 @@ class Batch:
         _check(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
         return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value}
 
+    def set_timing(self, on: bool = True):
+        """Record HIP events around every (uncaptured) step, for last_step_ms()."""
+        _check(self.L.ur3e_batch_set_timing(self.h, int(on)))
+
     def last_step_ms(self) -> float:
         ms = ctypes.c_float()
         _check(self.L.ur3e_batch_last_step_ms(self.h, ctypes.byref(ms)))
         return ms.value
 
 
-__all__ = ["Batch", "make_config", "load_model", "load_library", "TASK_GYM_V2", "TASK_TRAJ_L", "TASK_MOVE_J",
+__all__ = ["Batch", "make_config", "action_dim", "load_model", "load_library", "TASK_GYM_V2", "TASK_TRAJ_L", "TASK_MOVE_J",
            "TASK_CTRL", "TASK_GYM_V0", "TASK_IMIT_INDIRECT", "TASK_IMIT_DIRECT", "TASK_MOVE_L", "GAINS_L_MUG", "GAINS_V0",
            "GAINS_J", "GAINS_L_POS", "GAINS_L_ROT", "np"]
