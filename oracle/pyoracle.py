@@ -31,7 +31,7 @@ def lib():
     return _lib
 
 
-_SRCS = ("ur3e_oracle.c", "ur3e_oracle_batch.c")
+_SRCS = ("ur3e_oracle.c", "ur3e_oracle_batch.c", "ur3e_oracle_probe.c")
 
 
 def build_native(out_dir: str) -> str:
@@ -228,3 +228,68 @@ def philox(ctr, key):
     o = (ctypes.c_uint * 4)()
     L.ur3o_philox4x32(c, k, o)
     return list(o)
+
+
+class OracleData:
+    """One oracle mjData-like record (ur3o_data) for the physics known-answer and independent-solver
+    tests: set qpos/qvel/ctrl, run ur3o_forward / ur3o_step, read state, contacts and constraint rows
+    (oracle/ur3e_oracle_probe.c)."""
+
+    MAXC, MAXR = 64, 256
+
+    def __init__(self, model_c, L=None):
+        self.L = lib() if L is None else L
+        self.m = model_c
+        self.nq, self.nv, self.nu = model_c.nq, model_c.nv, model_c.nu
+        self.buf = ctypes.create_string_buffer(self.L.ur3o_sizeof_data())
+        self.L.ur3o_data_init(ctypes.byref(self.m), self.buf)
+
+    def set(self, qpos=None, qvel=None, ctrl=None, warm=None):
+        a = [None if x is None else np.ascontiguousarray(x, dtype=np.float64) for x in (qpos, qvel, ctrl)]
+        self.L.ur3o_data_set(ctypes.byref(self.m), self.buf, *[_p(x) for x in a])
+        if warm is not None:
+            w = np.ascontiguousarray(warm, dtype=np.float64)
+            self.L.ur3o_data_set_warmstart(ctypes.byref(self.m), self.buf, _p(w))
+
+    def forward(self):
+        self.L.ur3o_forward(ctypes.byref(self.m), self.buf)
+
+    def step(self, n=1):
+        for _ in range(n):
+            self.L.ur3o_step(ctypes.byref(self.m), self.buf)
+
+    def state(self):
+        nv = self.nv
+        out = dict(qpos=np.zeros(self.nq), qvel=np.zeros(nv), qacc=np.zeros(nv), qacc_smooth=np.zeros(nv),
+                   qfrc_smooth=np.zeros(nv), qM=np.zeros((nv, nv)))
+        self.L.ur3o_data_get(ctypes.byref(self.m), self.buf, *[_p(out[k]) for k in
+                                                                ("qpos", "qvel", "qacc", "qacc_smooth",
+                                                                 "qfrc_smooth", "qM")])
+        out["niter"] = self.L.ur3o_data_niter(self.buf)
+        return out
+
+    def contacts(self):
+        C = self.MAXC
+        pos, frame, dist = np.zeros((C, 3)), np.zeros((C, 9)), np.zeros(C)
+        geoms, fr, mu, adr = np.zeros((C, 2), np.int32), np.zeros((C, 5)), np.zeros(C), np.zeros(C, np.int32)
+        n = self.L.ur3o_data_contacts(self.buf, C, _p(pos), _p(frame), _p(dist), _p(geoms), _p(fr), _p(mu), _p(adr))
+        n = min(n, C)
+        return dict(n=n, pos=pos[:n], frame=frame[:n].reshape(n, 3, 3), dist=dist[:n], geoms=geoms[:n],
+                    friction=fr[:n], mu=mu[:n], efc_address=adr[:n])
+
+    def efc(self):
+        R_, nv = self.MAXR, self.nv
+        ints = {k: np.zeros(R_, np.int32) for k in ("type", "id", "state")}
+        J = np.zeros((R_, nv))
+        dbl = {k: np.zeros(R_) for k in ("pos", "margin", "frictionloss", "diagApprox", "R", "D", "vel", "aref",
+                                          "force")}
+        n = self.L.ur3o_data_efc(ctypes.byref(self.m), self.buf, R_, _p(ints["type"]), _p(ints["id"]),
+                                 _p(ints["state"]), _p(J), *[_p(dbl[k]) for k in
+                                                             ("pos", "margin", "frictionloss", "diagApprox", "R",
+                                                              "D", "vel", "aref", "force")])
+        n = min(n, R_)
+        out = {k: v[:n] for k, v in ints.items()}
+        out.update({k: v[:n] for k, v in dbl.items()})
+        out["J"] = J[:n]
+        out["n"] = n
+        return out
