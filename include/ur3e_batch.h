@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 3
+#define UR3E_ABI_VERSION 4
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -94,6 +94,10 @@ typedef struct ur3e_config_t {
   double rot_joint_gains[12]; /* kp[6], kd[6] of the rotation PD in move_l (config_l.yml "rot") */
   int np_chunk_lanes;    /* diagnostic (0 = 16): survivor lanes per compact-tier narrowphase chunk;
                             smaller values exercise its multi-chunk path */
+  int sensors;           /* 1: compute mjData.sensordata every forward (touch, actuatorfrc, torque via
+                            mj_rnePostConstraint; assets/main.xml:384-405) for ur3e_batch_get_sensordata.
+                            The torque sensors need the full-capacity layout, so the handle runs the
+                            full-capacity tier (envs_per_block 0 -> 128 lanes per env; > 0 rejected) */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;
@@ -136,6 +140,13 @@ int ur3e_batch_get_carry(ur3e_batch_t* b, double* d_carry, void* stream);
    d_touch [N, ntouch]; replaces d.sensordata reads in controller/move_l_mug.py:79 via
    utils/utils.py:238-240 (get_boolean_grasp_contact) */
 int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream);
+
+/* mjData.sensordata of the last forward, d_sensordata [N, model nsensordata] in the model's sensor
+   declaration order (main.xml: 6 torque x3, 6 arm actuatorfrc, right/left pad touch, fingers
+   actuatorfrc = 27 values); needs ur3e_config_t.sensors = 1.  Replaces d.sensor(name).data reads:
+   get_jnt_torques (utils/utils.py:201-211, called at controller/move_l_mug.py:80) and
+   get_grasp_contact (utils/utils.py:238-245) */
+int ur3e_batch_get_sensordata(ur3e_batch_t* b, double* d_sensordata, void* stream);
 
 /* d.ctrl after the last step, d_ctrl [N, nu]: the controller output the step applied (pid_task_ctrl
    torques + grip, PD torques, or the raw action); zero after a reset, like mj_resetData.  Replaces the

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define UR3E_MODEL_VERSION 4
+#define UR3E_MODEL_VERSION 5
 
 #define UR3E_MAXBODY 28
 #define UR3E_MAXJNT 16
@@ -35,6 +35,8 @@ extern "C" {
 #define UR3E_MAXTENWRAP 4
 #define UR3E_MAXKEY 2
 #define UR3E_MAXTOUCH 4
+#define UR3E_MAXSENSOR 16
+#define UR3E_MAXSENSORDATA 48
 
 /* per-env dynamic capacities (the kernels size scratch from these) */
 #define UR3E_MAXCON 40                                   /* contacts per env (main.xml: nconmax 100) */
@@ -61,6 +63,11 @@ extern "C" {
 #define UR3E_GAIN_FIXED 0
 #define UR3E_BIAS_NONE 0
 #define UR3E_BIAS_AFFINE 1
+
+/* sensor types (the subset main.xml declares, assets/main.xml:384-405) */
+#define UR3E_SENS_TOUCH 0       /* 1 value: normal force of contacts in the site volume */
+#define UR3E_SENS_ACTUATORFRC 1 /* 1 value: actuator_force */
+#define UR3E_SENS_TORQUE 2      /* 3 values: cfrc_int torque at the site, site frame (mj_rnePostConstraint) */
 
 /* cone */
 #define UR3E_CONE_PYRAMIDAL 0
@@ -201,6 +208,11 @@ typedef struct ur3e_model_t {
   int id_body_table;
   /* get_body_size(m, "fish")[-1]: half height of the first fish geom (ur3e_env.py compute_reward) */
   double fish_half_z;
+  /* all sensors in declaration order: mjData.sensordata[sensor_adr[k] ..] holds sensor k */
+  int nsensor, nsensordata;
+  int sensor_type[UR3E_MAXSENSOR];
+  int sensor_objid[UR3E_MAXSENSOR]; /* site (touch, torque) or actuator (actuatorfrc) */
+  int sensor_adr[UR3E_MAXSENSOR];
 } ur3e_model_t;
 
 #ifdef __cplusplus

@@ -59,7 +59,7 @@ class OracleConfig(ctypes.Structure):
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
         ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
-        ("np_chunk_lanes", ctypes.c_int),
+        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int),
     ]
 
 
@@ -119,6 +119,16 @@ class OracleBatch:
         warm = None if warm is None else np.ascontiguousarray(warm, dtype=np.float64)
         self.L.ur3o_batch_set_state(ctypes.byref(self.m), ctypes.c_int(self.n), self.buf, _p(qpos), _p(qvel),
                                     _p(warm))
+
+    def sensordata(self):
+        """[n, nsensordata] mjData.sensordata of every env's last forward"""
+        nsd = self.m.nsensordata
+        out = np.zeros((self.n, max(nsd, 1)))
+        sz = self.L.ur3o_sizeof_env()
+        for i in range(self.n):
+            ptr = ctypes.cast(ctypes.addressof(self.buf) + sz * i, ctypes.c_void_p)
+            self.L.ur3o_env_sensordata(ctypes.byref(self.m), ptr, _p(out[i]))
+        return out[:, :nsd]
 
     def diag(self, i):
         ncon, nefc, nit = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -266,6 +276,18 @@ class OracleData:
                                                                 ("qpos", "qvel", "qacc", "qacc_smooth",
                                                                  "qfrc_smooth", "qM")])
         out["niter"] = self.L.ur3o_data_niter(self.buf)
+        return out
+
+    def sensordata(self):
+        out = np.zeros(max(self.m.nsensordata, 1))
+        self.L.ur3o_data_sensordata(ctypes.byref(self.m), self.buf, _p(out))
+        return out[:self.m.nsensordata]
+
+    def rnepost(self):
+        nb = self.m.nbody
+        out = {k: np.zeros((nb, 6)) for k in ("cacc", "cfrc_int", "cfrc_ext")}
+        self.L.ur3o_data_rnepost(ctypes.byref(self.m), self.buf, _p(out["cacc"]), _p(out["cfrc_int"]),
+                                 _p(out["cfrc_ext"]))
         return out
 
     def contacts(self):

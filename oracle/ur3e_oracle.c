@@ -1409,6 +1409,140 @@ static void sensor_touch(const ur3e_model_t* m, ur3o_data* d) {
 }
 
 /* ===================================================================== */
+/* mj_rnePostConstraint + mj_sensorAcc (actuatorfrc, torque)              */
+/* ===================================================================== */
+/* mju_mulDofVec: res = sum_j mat[j] * vec[j] over n dof rows (n == 1: a scaled copy; MuJoCo's
+   mju_mulMatTVec skips zero multipliers) */
+static void mul_dof_vec(double res[6], const double (*mat)[6], const double* vec, int n) {
+  if (n == 1) {
+    for (int k = 0; k < 6; k++) res[k] = mat[0][k] * vec[0];
+    return;
+  }
+  for (int k = 0; k < 6; k++) res[k] = 0;
+  for (int j = 0; j < n; j++) {
+    double t = vec[j];
+    if (t == 0) continue;
+    for (int k = 0; k < 6; k++) res[k] += mat[j][k] * t;
+  }
+}
+
+/* mju_transformSpatial for a force vector [torque; force]: move the torque's reference point from
+   oldpos to newpos, then (rot != NULL) rotate both halves into the frame `rot` (new -> old) */
+static void transform_force(double res[6], const double vec[6], const double newpos[3], const double oldpos[3],
+                            const double* rot) {
+  double dif[3] = {newpos[0] - oldpos[0], newpos[1] - oldpos[1], newpos[2] - oldpos[2]};
+  double cros[3], tran[6];
+  cross3(cros, dif, vec + 3);
+  tran[0] = vec[0] - cros[0]; tran[1] = vec[1] - cros[1]; tran[2] = vec[2] - cros[2];
+  tran[3] = vec[3]; tran[4] = vec[4]; tran[5] = vec[5];
+  if (rot) {
+    mat_t_vec3(res, rot, tran);
+    mat_t_vec3(res + 3, rot, tran + 3);
+  } else {
+    for (int k = 0; k < 6; k++) res[k] = tran[k];
+  }
+}
+
+/* MuJoCo 3.3.3 mj_rnePostConstraint: body accelerations and interaction forces after the
+   constraint solve; external forces from contacts (elliptic: mj_contactForce = efc_force of the
+   cone rows, no torque for condim 3) and connect equalities (force at the anchors) */
+static void rne_post_constraint(const ur3e_model_t* m, ur3o_data* d) {
+  int nb = m->nbody;
+  for (int k = 0; k < 6; k++) d->cacc[0][k] = 0;
+  d->cacc[0][3] = m->gravity[0] * -1; d->cacc[0][4] = m->gravity[1] * -1; d->cacc[0][5] = m->gravity[2] * -1;
+  for (int i = 0; i < nb; i++)
+    for (int k = 0; k < 6; k++) d->cfrc_ext[i][k] = 0;
+  double cfrc[6], com[6];
+  for (int ci = 0; ci < d->ncon; ci++) {
+    const ur3o_contact* c = d->contact + ci;
+    if (c->efc_address < 0) continue;
+    double lfrc[3] = {d->efc_force[c->efc_address], d->efc_force[c->efc_address + 1],
+                      d->efc_force[c->efc_address + 2]};
+    double zero[3] = {0, 0, 0};
+    mat_t_vec3(cfrc, c->frame, zero);
+    mat_t_vec3(cfrc + 3, c->frame, lfrc);
+    int k = m->geom_bodyid[c->geom1];
+    if (k) {
+      transform_force(com, cfrc, d->subtree_com[m->body_rootid[k]], c->pos, 0);
+      for (int r = 0; r < 6; r++) d->cfrc_ext[k][r] -= com[r];
+    }
+    k = m->geom_bodyid[c->geom2];
+    if (k) {
+      transform_force(com, cfrc, d->subtree_com[m->body_rootid[k]], c->pos, 0);
+      for (int r = 0; r < 6; r++) d->cfrc_ext[k][r] += com[r];
+    }
+  }
+  /* equality rows lead the constraint list (make_constraint) */
+  int i = 0;
+  while (i < d->nefc && d->efc_type[i] == UR3O_CNSTR_EQUALITY) {
+    int e = d->efc_id[i];
+    if (m->eq_type[e] == UR3E_EQ_CONNECT) {
+      cfrc[0] = cfrc[1] = cfrc[2] = 0;
+      cfrc[3] = d->efc_force[i]; cfrc[4] = d->efc_force[i + 1]; cfrc[5] = d->efc_force[i + 2];
+      for (int side = 0; side < 2; side++) {
+        int k = side == 0 ? m->eq_obj1[e] : m->eq_obj2[e];
+        if (!k) continue;
+        double pos[3];
+        mat_vec3(pos, d->xmat[k], m->eq_data[e] + 3 * side);
+        pos[0] += d->xpos[k][0]; pos[1] += d->xpos[k][1]; pos[2] += d->xpos[k][2];
+        transform_force(com, cfrc, d->subtree_com[m->body_rootid[k]], pos, 0);
+        if (side == 0)
+          for (int r = 0; r < 6; r++) d->cfrc_ext[k][r] += com[r];
+        else
+          for (int r = 0; r < 6; r++) d->cfrc_ext[k][r] -= com[r];
+      }
+      i += 3;
+    } else {
+      i++;
+    }
+  }
+  for (int b = 1; b < nb; b++) {
+    int bda = m->body_dofadr[b], n = m->body_dofnum[b];
+    double tmp[6], tmp1[6];
+    if (n > 0) mul_dof_vec(tmp, (const double(*)[6])d->cdof_dot[bda], d->qvel + bda, n);
+    else for (int k = 0; k < 6; k++) tmp[k] = 0;
+    int p = m->body_parentid[b];
+    for (int k = 0; k < 6; k++) d->cacc[b][k] = d->cacc[p][k] + tmp[k];
+    if (n > 0) mul_dof_vec(tmp, (const double(*)[6])d->cdof[bda], d->qacc + bda, n);
+    else for (int k = 0; k < 6; k++) tmp[k] = 0;
+    for (int k = 0; k < 6; k++) d->cacc[b][k] += tmp[k];
+    mul_inert_vec(d->cfrc_int[b], d->cinert[b], d->cacc[b]);
+    mul_inert_vec(tmp, d->cinert[b], d->cvel[b]);
+    cross_force(tmp1, d->cvel[b], tmp);
+    for (int k = 0; k < 6; k++) d->cfrc_int[b][k] += tmp1[k];
+    for (int k = 0; k < 6; k++) d->cfrc_int[b][k] -= d->cfrc_ext[b][k];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p)
+      for (int k = 0; k < 6; k++) d->cfrc_int[p][k] += d->cfrc_int[b][k];
+  }
+}
+
+/* mjData.sensordata in declaration order (touch from sensor_touch) */
+static void sensors(const ur3e_model_t* m, ur3o_data* d) {
+  int post = 0;
+  for (int k = 0; k < m->nsensor; k++) post |= m->sensor_type[k] == UR3E_SENS_TORQUE;
+  if (post) rne_post_constraint(m, d);
+  int nt = 0;
+  for (int k = 0; k < m->nsensor; k++) {
+    double* out = d->sensordata + m->sensor_adr[k];
+    int obj = m->sensor_objid[k];
+    if (m->sensor_type[k] == UR3E_SENS_TOUCH) {
+      out[0] = d->touch[nt++];
+    } else if (m->sensor_type[k] == UR3E_SENS_ACTUATORFRC) {
+      out[0] = d->actuator_force[obj];
+    } else {
+      int body = m->site_bodyid[obj];
+      double res[6];
+      transform_force(res, d->cfrc_int[body], d->site_xpos[obj], d->subtree_com[m->body_rootid[body]],
+                      d->site_xmat[obj]);
+      out[0] = res[0]; out[1] = res[1]; out[2] = res[2];
+    }
+  }
+}
+
+/* ===================================================================== */
 /* forward / step                                                         */
 /* ===================================================================== */
 void ur3o_reset_data(const ur3e_model_t* m, ur3o_data* d) {
@@ -1444,6 +1578,7 @@ void ur3o_forward(const ur3e_model_t* m, ur3o_data* d) {
   /* constraint solve */
   solve_newton(m, d);
   sensor_touch(m, d);
+  sensors(m, d);
 }
 
 static int is_bad(double x) { return x != x || x > MAXVAL || x < -MAXVAL; }

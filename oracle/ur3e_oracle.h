@@ -123,6 +123,9 @@ typedef struct {
   double qfrc_constraint[UR3E_MAXNV];
   double qacc[UR3E_MAXNV];
   double touch[UR3E_MAXTOUCH];
+  /* mj_rnePostConstraint (only when the model has torque sensors) and mjData.sensordata */
+  double cacc[UR3E_MAXBODY][6], cfrc_int[UR3E_MAXBODY][6], cfrc_ext[UR3E_MAXBODY][6];
+  double sensordata[UR3E_MAXSENSORDATA];
   int solver_niter;
   int nwarning_bad;
 } ur3o_data;

@@ -49,6 +49,7 @@ typedef struct {
   int tier_con_cap;
   double rot_joint_gains[12];
   int np_chunk_lanes; /* GPU-tier diagnostic, unused here (layout mirror of ur3e_config_t) */
+  int sensors;        /* the oracle always computes sensordata (layout mirror) */
 } ur3o_config;
 
 /* the model has the sites the 24-d observation reads (main.xml) */
@@ -235,6 +236,10 @@ void ur3o_env_diag(const ur3o_env* e, int* ncon, int* nefc, int* niter, double* 
 }
 
 /* d.ctrl applied by the last step (UR3E_MAXU entries) */
+void ur3o_env_sensordata(const ur3e_model_t* m, const ur3o_env* e, double* out) {
+  for (int k = 0; k < m->nsensordata; k++) out[k] = e->d.sensordata[k];
+}
+
 void ur3o_env_ctrl(const ur3o_env* e, double* ctrl) {
   for (int k = 0; k < UR3E_MAXU; k++) ctrl[k] = e->d.ctrl[k];
 }

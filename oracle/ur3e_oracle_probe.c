@@ -83,3 +83,15 @@ int ur3o_data_efc(const ur3e_model_t* m, const ur3o_data* d, int maxr, int* type
 }
 
 int ur3o_data_niter(const ur3o_data* d) { return d->solver_niter; }
+
+void ur3o_data_sensordata(const ur3e_model_t* m, const ur3o_data* d, double* out) {
+  memcpy(out, d->sensordata, sizeof(double) * m->nsensordata);
+}
+
+/* cfrc_int / cfrc_ext / cacc of the last forward's mj_rnePostConstraint, [nbody, 6] each */
+void ur3o_data_rnepost(const ur3e_model_t* m, const ur3o_data* d, double* cacc, double* cfrc_int,
+                       double* cfrc_ext) {
+  memcpy(cacc, d->cacc, sizeof(double) * 6 * m->nbody);
+  memcpy(cfrc_int, d->cfrc_int, sizeof(double) * 6 * m->nbody);
+  memcpy(cfrc_ext, d->cfrc_ext, sizeof(double) * 6 * m->nbody);
+}

@@ -38,3 +38,23 @@ class OracleStepper:
 
     def close(self):
         pass
+
+
+def oracle_pick_place_rows(md, mc, ob):
+    """Per-env build_traj_l_pick_place rows [n, 7200, 7] for an OracleBatch created with the
+    move_l_mug configuration (controller/move_l_mug.py:36-38: start = tcp pose, pick = handle_site,
+    place = ghost, rotation held at the start's rotvec), from the oracle's reset state."""
+    from scipy.spatial.transform import Rotation as R
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.build_traj import build_traj_l_pick_place
+    qp = ob.get_state()[0]
+    tcp, h = md["id_site_tcp"], md["id_site_handle"]
+    rows = []
+    for i in range(ob.n):
+        fs = po.forward_state(mc, qp[i])
+        rv = R.from_matrix(fs["site_xmat"][tcp].reshape(3, 3)).as_rotvec()
+        start = np.r_[fs["site_xpos"][tcp], rv, 0.0]
+        pick = np.r_[fs["site_xpos"][h], rv, 0.5]
+        place = np.r_[ob.obs[i, 6:9], rv, 1.0]
+        rows.append(build_traj_l_pick_place(start, [pick, place]))
+    return np.stack(rows)

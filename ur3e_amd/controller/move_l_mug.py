@@ -47,7 +47,9 @@ class MoveLMug:
     """N scripted pick-and-place episodes stepping in lock-step."""
 
     def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
-                 envs_per_block: int = 0):
+                 envs_per_block: int = 0, sensors: bool = False):
+        """sensors=True also records mjData.sensordata every row (actuator_frc[t] = get_jnt_torques(d),
+        move_l_mug.py:80), at the cost of the full-capacity kernel (see ur3e_config_t.sensors)."""
         import torch
         from .. import runtime as rt
         self.torch = torch
@@ -55,7 +57,7 @@ class MoveLMug:
         self.md = md
         cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
                              reset_noise=NOISE[reset_mode], reset_key=md["id_key_down"], model=md, seed=seed,
-                             envs_per_block=envs_per_block)
+                             envs_per_block=envs_per_block, sensors=sensors)
         self.batch = rt.Batch(mc, cfg, n_envs, device=device)   # reset_with_mug (keyframe + forward)
         obs = self.batch.obs
         start = task_space_state(self.batch)
@@ -87,6 +89,16 @@ class MoveLMug:
             if record_every and self.t % record_every == 0:
                 rec[self.t] = task_space_state(self.batch)
         return rec
+
+    def actuator_frc(self):
+        """[N, 7] get_jnt_torques (utils/utils.py:201-211): the 7 actuatorfrc sensors by name order"""
+        md = self.md
+        names = ["shoulder_pan_motor", "shoulder_lift_motor", "elbow_motor", "wrist_1_motor", "wrist_2_motor",
+                 "wrist_3_motor", "fingers_actuator"]
+        act = {nm: k for k, nm in enumerate(md["act_names"])}
+        adr = {md["sensor_objid"][j]: md["sensor_adr"][j] for j in range(md["nsensor"]) if md["sensor_type"][j] == 1}
+        sd = self.batch.get_sensordata()
+        return sd[:, [adr[act[nm]] for nm in names]]
 
     def close(self):
         self.batch.close()

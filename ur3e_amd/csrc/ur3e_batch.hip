@@ -384,6 +384,7 @@ struct KState {
   int* nwarn;
   double* touch; /* [env][UR3E_MAXTOUCH] touch sensors after the last forward */
   double* ctrl;  /* [env][UR3E_MAXU] d.ctrl after the last step (the controller output it applied) */
+  double* sensordata; /* [env][UR3E_MAXSENSORDATA] mjData.sensordata of the last forward (sensors on) */
 };
 
 struct KConfig {
@@ -394,6 +395,7 @@ struct KConfig {
   int tier_con_cap;
   int np_lanes; /* survivor lanes per compact narrowphase chunk (1..W_NP_LANES) */
   int obs_sites; /* model has tcp / handle_site / ghost: the scripted tasks also emit the 24-d obs */
+  int sensors;   /* compute and store mjData.sensordata every forward (full-capacity kernels) */
   KGains gains;
 };
 
@@ -832,6 +834,7 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
     s.ovf = 0;
     s.cap_con = (KS::BAIL && c.tier_con_cap > 0 && c.tier_con_cap < KS::MAXCON) ? c.tier_con_cap : KS::MAXCON;
     if constexpr (KS::OVERLAY) s.np_lanes = c.np_lanes;
+    else s.sens = c.sensors;
     o.t = st.t[e]; o.ep_len = st.ep_len[e]; o.ep_return = st.ep_return[e]; o.episode = st.episode[e];
     o.did_reset = 0; o.term = 0; o.trunc = 0; o.r = 0;
   }
@@ -847,6 +850,11 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
   for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
   for (int k = tid; k < m->nu; k += NT) st.ctrl[(size_t)e * UR3E_MAXU + k] = s.ctrl[k];
+  if constexpr (!KS::OVERLAY) {
+    if (c.sensors)
+      for (int k = tid; k < m->nsensordata; k += NT)
+        st.sensordata[(size_t)e * UR3E_MAXSENSORDATA + k] = s.sensordata[k];
+  }
   const int od = k_obs_dim(c.task);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
@@ -1382,7 +1390,12 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   if (cfg->envs_per_block > 64) return fail(UR3E_EINVAL, "envs_per_block > 64");
   /* 0: two-tier (default); -64: full-capacity tier, 64 lanes; other negative: full-capacity tier,
      128 lanes; 1..64: v1 lane-per-env */
-  int tiered = cfg->envs_per_block == 0;
+  if (cfg->sensors && cfg->envs_per_block > 0)
+    return fail(UR3E_EINVAL, "sensors need a workgroup-per-env layout (envs_per_block <= 0)");
+  if (cfg->sensors && model->nsensordata > UR3E_MAXSENSORDATA) return fail(UR3E_EMODEL, "too much sensordata");
+  /* sensors: the torque sensors need mj_rnePostConstraint's body quantities after the solve, which
+     only the full-capacity layout keeps, so a handle with sensors on runs the full-capacity tier */
+  int tiered = cfg->envs_per_block == 0 && !cfg->sensors;
   int wave_nt = cfg->envs_per_block == 0 ? 128 : (cfg->envs_per_block == -64 ? 64 : (cfg->envs_per_block < 0 ? 128 : 0));
   if (wave_nt && model->ncpair > W_MAXCAND) return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
   HIPCHK(hipSetDevice(device));
@@ -1407,6 +1420,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.tier_con_cap = cfg->tier_con_cap;
   c.np_lanes = cfg->np_chunk_lanes > 0 && cfg->np_chunk_lanes < W_NP_LANES ? cfg->np_chunk_lanes : W_NP_LANES;
   c.obs_sites = model->id_site_tcp >= 0 && model->id_site_handle >= 0 && model->id_body_ghost >= 0;
+  c.sensors = cfg->sensors != 0;
   KPlan plan;
   build_plan(model, &plan);
   b->main_tree = model->nv == UR3E_MAIN_NV;
@@ -1443,6 +1457,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.touch, 0, sizeof(double) * nd * UR3E_MAXTOUCH));
   HIPCHK(hipMalloc(&s.ctrl, sizeof(double) * nd * UR3E_MAXU));
   HIPCHK(hipMemset(s.ctrl, 0, sizeof(double) * nd * UR3E_MAXU));
+  s.sensordata = nullptr;
+  if (c.sensors) {
+    HIPCHK(hipMalloc(&s.sensordata, sizeof(double) * nd * UR3E_MAXSENSORDATA));
+    HIPCHK(hipMemset(s.sensordata, 0, sizeof(double) * nd * UR3E_MAXSENSORDATA));
+  }
   HIPCHK(hipMemset(s.episode, 0, sizeof(unsigned int) * nd));
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
@@ -1467,6 +1486,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
                   b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->d_ovf_list, b->d_ovf_ctl,
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
+  if (b->st.sensordata) (void)hipFree(b->st.sensordata);
   (void)hipEventDestroy(b->ev0);
   (void)hipEventDestroy(b->ev1);
   delete b;
@@ -1613,6 +1633,23 @@ extern "C" int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream
   HIPCHK(hipSetDevice(b->device));
   hipLaunchKernelGGL(k_env_get_ctrl, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
                      b->host_model.nu, d_ctrl);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+__global__ void k_env_get_sensordata(KState s, int nsd, double* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  for (int k = 0; k < nsd; k++) out[(size_t)e * nsd + k] = s.sensordata[(size_t)e * UR3E_MAXSENSORDATA + k];
+}
+
+extern "C" int ur3e_batch_get_sensordata(ur3e_batch_t* b, double* d_sensordata, void* stream) {
+  if (!b || !d_sensordata) return fail(UR3E_EINVAL, "null argument");
+  if (!b->cfg.sensors) return fail(UR3E_EINVAL, "sensors are off (ur3e_config_t.sensors = 0)");
+  HIPCHK(hipSetDevice(b->device));
+  if (b->host_model.nsensordata > 0)
+    hipLaunchKernelGGL(k_env_get_sensordata, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
+                       b->host_model.nsensordata, d_sensordata);
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }

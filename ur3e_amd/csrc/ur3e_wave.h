@@ -118,6 +118,10 @@ struct KSX<MC, ME, NVC, TREE, false> {
   int efc_type[ME], efc_id[ME], efc_state[ME], rowflag[ME], efc_grp[ME];
   int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
   double touch[UR3E_MAXTOUCH];
+  /* sensors (ur3e_config_t.sensors): mjData.sensordata and mj_rnePostConstraint's body quantities */
+  double sensordata[UR3E_MAXSENSORDATA];
+  double cacc[K_NB][6], cfrc_int[K_NB][6], cfrc_ext[K_NB][6];
+  int sens;
   /* scalars */
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
@@ -1698,6 +1702,156 @@ WD void w_solve_newton(KModel m, KS& s) {
 /* ================================================================== */
 /* forward / step                                                      */
 /* ================================================================== */
+/* sensors: mj_rnePostConstraint + mjData.sensordata (oracle rne_post_constraint / sensors), the   */
+/* full-capacity layout only -- the compact tier's overlaid LDS has no room for cinert/cvel/cdof_dot */
+/* after the solve, so a handle with sensors on runs the full-capacity kernels (ur3e_batch_create)  */
+/* ================================================================== */
+/* oracle transform_force: torque reference point oldpos -> newpos, then optionally into frame rot */
+KD void w_transform_force(double res[6], const double vec[6], const double newpos[3], const double oldpos[3],
+                          const double* rot) {
+  double dif[3] = {newpos[0] - oldpos[0], newpos[1] - oldpos[1], newpos[2] - oldpos[2]};
+  double cros[3], tran[6];
+  k_cross3(cros, dif, vec + 3);
+  tran[0] = vec[0] - cros[0]; tran[1] = vec[1] - cros[1]; tran[2] = vec[2] - cros[2];
+  tran[3] = vec[3]; tran[4] = vec[4]; tran[5] = vec[5];
+  if (rot) {
+    k_mat_t_vec3(res, rot, tran);
+    k_mat_t_vec3(res + 3, rot, tran + 3);
+  } else {
+    for (int k = 0; k < 6; k++) res[k] = tran[k];
+  }
+}
+
+template <int NT, class KS>
+WD void w_sensors(KModel m, const KPlan* __restrict__ pl, KS& s) {
+  if constexpr (!KS::OVERLAY) {
+    const int tid = w_lane();
+    const int nb = m->nbody;
+    int post = 0;
+    for (int k = 0; k < m->nsensor; k++) post |= m->sensor_type[k] == UR3E_SENS_TORQUE;
+    if (post) {
+      /* cfrc_ext, lane = body: every body sums its contributions in the oracle's order (contacts,
+         then the connect rows that lead the constraint list) */
+      for (int b = tid; b < nb; b += NT) {
+        double ext[6] = {0, 0, 0, 0, 0, 0};
+        if (b > 0) {
+          for (int ci = 0; ci < s.ncon; ci++) {
+            const int adr = s.con_efc[ci];
+            if (adr < 0) continue;
+            const int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+            if (b != b1 && b != b2) continue;
+            double lfrc[3] = {s.efc_force[adr], s.efc_force[adr + 1], s.efc_force[adr + 2]};
+            double zero[3] = {0, 0, 0};
+            double cfrc[6], com[6];
+            k_mat_t_vec3(cfrc, s.con_frame[ci], zero);
+            k_mat_t_vec3(cfrc + 3, s.con_frame[ci], lfrc);
+            if (b == b1) {
+              w_transform_force(com, cfrc, s.subtree_com[m->body_rootid[b]], s.con_pos[ci], 0);
+              for (int r = 0; r < 6; r++) ext[r] -= com[r];
+            }
+            if (b == b2) {
+              w_transform_force(com, cfrc, s.subtree_com[m->body_rootid[b]], s.con_pos[ci], 0);
+              for (int r = 0; r < 6; r++) ext[r] += com[r];
+            }
+          }
+          int i = 0;
+          while (i < s.nefc && s.efc_type[i] == CN_EQUALITY) {
+            const int e = s.efc_id[i];
+            if (m->eq_type[e] == UR3E_EQ_CONNECT) {
+              double cfrc[6] = {0, 0, 0, s.efc_force[i], s.efc_force[i + 1], s.efc_force[i + 2]};
+              for (int side = 0; side < 2; side++) {
+                const int k = side == 0 ? m->eq_obj1[e] : m->eq_obj2[e];
+                if (k != b) continue;
+                double pos[3], com[6];
+                k_mat_vec3(pos, s.xmat[k], m->eq_data[e] + 3 * side);
+                pos[0] += s.xpos[k][0]; pos[1] += s.xpos[k][1]; pos[2] += s.xpos[k][2];
+                w_transform_force(com, cfrc, s.subtree_com[m->body_rootid[k]], pos, 0);
+                if (side == 0)
+                  for (int r = 0; r < 6; r++) ext[r] += com[r];
+                else
+                  for (int r = 0; r < 6; r++) ext[r] -= com[r];
+              }
+              i += 3;
+            } else {
+              i++;
+            }
+          }
+        }
+        for (int r = 0; r < 6; r++) s.cfrc_ext[b][r] = ext[r];
+      }
+      /* cacc, lane = component: each component's tree sweep is serial in body order */
+      if (tid < 6) {
+        const int k = tid;
+        s.cacc[0][k] = k < 3 ? 0.0 : m->gravity[k - 3] * -1;
+        for (int b = 1; b < nb; b++) {
+          const int bda = m->body_dofadr[b], n = m->body_dofnum[b];
+          double t = 0;
+          if (n == 1) {
+            t = s.cdof_dot[bda][k] * s.qvel[bda];
+          } else if (n > 1) {
+            for (int j = 0; j < n; j++) {
+              const double v = s.qvel[bda + j];
+              if (v == 0) continue;
+              t += s.cdof_dot[bda + j][k] * v;
+            }
+          }
+          double c = s.cacc[m->body_parentid[b]][k] + t;
+          t = 0;
+          if (n == 1) {
+            t = s.cdof[bda][k] * s.qacc[bda];
+          } else if (n > 1) {
+            for (int j = 0; j < n; j++) {
+              const double a = s.qacc[bda + j];
+              if (a == 0) continue;
+              t += s.cdof[bda + j][k] * a;
+            }
+          }
+          s.cacc[b][k] = c + t;
+        }
+      }
+      SYNC();
+      /* cfrc_int before accumulation, lane = body */
+      for (int b = 1 + tid; b < nb; b += NT) {
+        double f[6], tmp[6], tmp1[6];
+        k_mul_inert_vec(f, s.cinert[b], s.cacc[b]);
+        k_mul_inert_vec(tmp, s.cinert[b], s.cvel[b]);
+        k_cross_force(tmp1, s.cvel[b], tmp);
+        for (int r = 0; r < 6; r++) f[r] += tmp1[r];
+        for (int r = 0; r < 6; r++) s.cfrc_int[b][r] = f[r] - s.cfrc_ext[b][r];
+      }
+      SYNC();
+      /* accumulate children into parents, lane = component, reverse body order */
+      if (tid < 6)
+        for (int b = nb - 1; b > 0; b--) {
+          const int p = m->body_parentid[b];
+          if (p) s.cfrc_int[p][tid] += s.cfrc_int[b][tid];
+        }
+      SYNC();
+    }
+    /* sensordata in declaration order, lane = sensor */
+    for (int k = tid; k < m->nsensor; k += NT) {
+      double* out = s.sensordata + m->sensor_adr[k];
+      const int obj = m->sensor_objid[k];
+      const int type = m->sensor_type[k];
+      if (type == UR3E_SENS_TOUCH) {
+        int nt = 0;
+        for (int j = 0; j < k; j++) nt += m->sensor_type[j] == UR3E_SENS_TOUCH;
+        out[0] = s.touch[nt];
+      } else if (type == UR3E_SENS_ACTUATORFRC) {
+        out[0] = s.act_force[obj];
+      } else {
+        const int body = m->site_bodyid[obj];
+        double res[6];
+        w_transform_force(res, s.cfrc_int[body], s.site_xpos[obj], s.subtree_com[m->body_rootid[body]],
+                          s.site_xmat[obj]);
+        out[0] = res[0]; out[1] = res[1]; out[2] = res[2];
+      }
+    }
+    SYNC();
+  }
+}
+
+/* ================================================================== */
 template <int NT, class KS>
 WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
@@ -1822,6 +1976,9 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
     s.touch[tid] = sum;
   }
   SYNC();
+  if constexpr (!KS::OVERLAY) {
+    if (s.sens) w_sensors<NT>(m, pl, s);
+  }
 }
 
 /* mj_step pieces around the forward pass, so a caller can keep ONE inlined copy of w_forward

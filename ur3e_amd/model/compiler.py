@@ -9,7 +9,7 @@ the MJCF features the three reference models use:
 * bodies (pos, quat), `<inertial>` (diaginertia + quat), hinge and free joints,
   geoms (plane, box, mesh -> surrogate box, see `surrogate.py`), sites;
 * `<contact>` `<exclude>` and `<pair>`, fixed tendons, equality connect/joint,
-  motor and general(affine) actuators, touch sensors, keyframes.
+  motor and general(affine) actuators, touch / actuatorfrc / torque sensors, keyframes.
 
 It also performs the `mj_setConst` work MuJoCo does at compile time
 (qpos0-based body/dof inverse weights, `meaninertia`, connect anchors in body2's
@@ -37,7 +37,9 @@ from .surrogate import DENSITY, MESH_SURROGATE
 MAXBODY, MAXJNT, MAXNQ, MAXNV = 28, 16, 24, 24
 MAXGEOM, MAXSITE, MAXCPAIR, MAXEQ = 32, 20, 320, 4
 MAXU, MAXTEN, MAXTENWRAP, MAXKEY, MAXTOUCH = 8, 2, 4, 2, 4
-MODEL_VERSION = 4
+MAXSENSOR = 16
+MODEL_VERSION = 5
+SENS_TOUCH, SENS_ACTUATORFRC, SENS_TORQUE = 0, 1, 2
 
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = 0, 1, 2, 3
 GEOM_PLANE, GEOM_BOX = 0, 6
@@ -499,13 +501,31 @@ def compile_mjcf(path: str) -> dict:
             else:
                 raise ValueError(f"unsupported equality {ch.tag}")
 
-    # ---------------- sensors (touch only feed the hot path)
+    # ---------------- sensors, in declaration order (mjData.sensordata layout): touch (1 value, site),
+    # actuatorfrc (1, actuator), torque (3, site; needs mj_rnePostConstraint)
     touch = []
+    sens_type, sens_obj, sens_adr = [], [], []
+    act_names = {a["name"]: k for k, a in enumerate(acts)}
+    nsd = 0
     se = root.find("sensor")
     if se is not None:
         for ch in se:
+            if not isinstance(ch.tag, str):
+                continue
             if ch.tag == "touch":
-                touch.append(names["site"][ch.get("site")])
+                obj = names["site"][ch.get("site")]
+                touch.append(obj)
+                t, dim = SENS_TOUCH, 1
+            elif ch.tag == "actuatorfrc":
+                obj, t, dim = act_names[ch.get("actuator")], SENS_ACTUATORFRC, 1
+            elif ch.tag == "torque":
+                obj, t, dim = names["site"][ch.get("site")], SENS_TORQUE, 3
+            else:
+                raise ValueError(f"unsupported sensor {ch.tag}")
+            sens_type.append(t)
+            sens_obj.append(obj)
+            sens_adr.append(nsd)
+            nsd += dim
 
     # ---------------- keyframes
     keys = {}
@@ -567,6 +587,8 @@ def compile_mjcf(path: str) -> dict:
         act_gainprm=[a["gain"] for a in acts], act_biasprm=[a["bias"] for a in acts],
         act_gear=[a["gear"] for a in acts], act_names=[a["name"] for a in acts],
         touch_site=touch,
+        nsensor=len(sens_type), nsensordata=nsd, sensor_type=sens_type, sensor_objid=sens_obj,
+        sensor_adr=sens_adr,
         key_names=key_names,
         key_qpos=[keys[k][0].tolist() for k in key_names], key_qvel=[keys[k][1].tolist() for k in key_names],
         body_names=[b["name"] for b in bodies], joint_names=[j["name"] for j in joints],
@@ -909,6 +931,8 @@ class UR3eModelC(ctypes.Structure):
         ("fish_topple_z", _d),
         ("id_body_table", _i),
         ("fish_half_z", _d),
+        ("nsensor", _i), ("nsensordata", _i), ("sensor_type", _i * MAXSENSOR), ("sensor_objid", _i * MAXSENSOR),
+        ("sensor_adr", _i * MAXSENSOR),
     ]
 
 

@@ -48,7 +48,7 @@ class ConfigC(ctypes.Structure):
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
         ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
-        ("np_chunk_lanes", ctypes.c_int),
+        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int),
     ]
 
 
@@ -75,6 +75,7 @@ def load_library():
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
+    L.ur3e_batch_get_sensordata.argtypes = [vp, vp, vp]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim"):
         getattr(L, f).argtypes = [vp]
     _lib = L
@@ -96,7 +97,7 @@ def load_model(name: str = "main"):
 def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
                 reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
                 task_gains=None, joint_gains=None, tier_con_cap=0, rot_joint_gains=None,
-                np_chunk_lanes=0) -> ConfigC:
+                np_chunk_lanes=0, sensors=False) -> ConfigC:
     c = ConfigC()
     c.task = task
     c.frame_skip = frame_skip
@@ -123,6 +124,7 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.envs_per_block = envs_per_block
     c.tier_con_cap = tier_con_cap
     c.np_chunk_lanes = np_chunk_lanes
+    c.sensors = int(sensors)
     return c
 
 
@@ -224,6 +226,14 @@ class Batch:
         out = self.torch.empty((self.n, self.nu), dtype=self.torch.float64, device=self.device)
         _check(self.L.ur3e_batch_get_ctrl(self.h, _ptr(out), self._stream()))
         return out
+
+    def get_sensordata(self):
+        """[N, nsensordata] mjData.sensordata of the last forward (config sensors=True), in the model's
+        sensor declaration order (sensor_names / sensor_adr of the model dict)"""
+        nsd = self.model_c.nsensordata
+        out = self.torch.zeros((self.n, max(nsd, 1)), dtype=self.torch.float64, device=self.device)
+        _check(self.L.ur3e_batch_get_sensordata(self.h, _ptr(out), self._stream()))
+        return out[:, :nsd]
 
     def get_carry(self):
         """[N, 54] stale-kinematics snapshot: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6]."""
