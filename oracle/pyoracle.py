@@ -59,7 +59,7 @@ class OracleConfig(ctypes.Structure):
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
         ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
-        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int),
+        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int), ("schedule", ctypes.c_int),
     ]
 
 

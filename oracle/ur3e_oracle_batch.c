@@ -50,6 +50,7 @@ typedef struct {
   double rot_joint_gains[12];
   int np_chunk_lanes; /* GPU-tier diagnostic, unused here (layout mirror of ur3e_config_t) */
   int sensors;        /* the oracle always computes sensordata (layout mirror) */
+  int schedule;       /* GPU launch schedule, unused here (layout mirror) */
 } ur3o_config;
 
 /* the model has the sites the 24-d observation reads (main.xml) */

@@ -177,3 +177,37 @@ def test_sharded_envs_rccl_self_gather(env_id):
         plain.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,cap", [(777, 0), (4096, 0), (512, 3)])
+def test_substep_queue_matches_env_step_launch(n, cap):
+    """The default two-tier launch of a gym step with frame_skip 2 is the substep work queue
+    (w_env_step_q: (substep, env) units, state handed over through HBM between substeps).  It must
+    equal the one-workgroup-per-env-step launch (schedule 1) bit for bit, every step, including
+    envs that bail to the full-capacity tier in either substep (cap = diagnostic contact cap) and
+    auto-resets; n = 777 is not a multiple of the 8 XCDs."""
+    torch = _torch()
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model("main")
+    kw = dict(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=17, max_episode_steps=40, tier_con_cap=cap)
+    gq = rt.Batch(mc, rt.make_config(schedule=0, **kw), n)
+    ge = rt.Batch(mc, rt.make_config(schedule=1, **kw), n)
+    _eq(torch, gq.obs, ge.obs, "reset obs")
+    rng = np.random.default_rng(8)
+    for s in range(60):
+        a = _grasp_actions(rng, n) if s % 3 else rng.uniform(LO, HI, size=(n, 4))
+        at = torch.from_numpy(a).cuda()
+        q = gq.step(at)
+        e = ge.step(at)
+        for x, y, what in zip(q[:4], e[:4], ("obs", "reward", "terminated", "truncated")):
+            _eq(torch, x, y, f"{what} step {s}")
+        done = (e[2] | e[3]) > 0
+        _eq(torch, q[4][done], e[4][done], f"terminal obs step {s}")
+    for x, y, what in zip(gq.get_state(), ge.get_state(), ("qpos", "qvel", "warmstart")):
+        _eq(torch, x, y, what)
+    _eq(torch, gq.get_info()["ncon"], ge.get_info()["ncon"], "ncon")
+    oq, oe = gq.overflow_count(), ge.overflow_count()
+    if cap:
+        assert oq > 0 and oe > 0
+    gq.close()
+    ge.close()

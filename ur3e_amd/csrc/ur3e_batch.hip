@@ -799,7 +799,7 @@ KD int k_termination_v0(KModel m, const double obs[13], int selfcol) {
   return 0;
 }
 
-KD int k_is_gym(int task) {
+__host__ __device__ static inline int k_is_gym(int task) {
   return task == UR3E_TASK_GYM_V2 || (task >= UR3E_TASK_GYM_V0 && task <= UR3E_TASK_IMIT_DIRECT);
 }
 __host__ __device__ static inline int k_obs_dim(int task) { return (task == UR3E_TASK_GYM_V0 || task == UR3E_TASK_IMIT_DIRECT) ? 13 : 24; }
@@ -917,18 +917,54 @@ WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, in
   w_reset_finish<NT>(m, pl, c, s, o);
 }
 
-/* one env-step of env e into LDS (s, o); false: the compact tier overflowed */
+/* mid-step state of an env between the substep units of the queued step kernel (w_env_step_q):
+   qpos, qvel, qacc_warmstart after the unit's last Euler update, the applied ctrl and the warning
+   count -- everything the next substep reads that is not in the env's committed state */
+#define W_MID_QPOS 0
+#define W_MID_QVEL K_NQ
+#define W_MID_WARM (K_NQ + K_NV)
+#define W_MID_CTRL (K_NQ + 2 * K_NV)
+#define W_MID_NWARN (K_NQ + 2 * K_NV + K_NU)
+#define W_MID (((W_MID_NWARN + 1) + 7) / 8 * 8)
+
 template <int NT, class KS>
-WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
-                        const double* __restrict__ actions, int adim, KS& s, WOut& o) {
+WD void w_store_mid(KModel m, double* __restrict__ mid, int e, const KS& s) {
+  const int tid = w_lane();
+  double* p = mid + (size_t)e * W_MID;
+  for (int k = tid; k < m->nq; k += NT) p[W_MID_QPOS + k] = s.qpos[k];
+  for (int k = tid; k < m->nv; k += NT) { p[W_MID_QVEL + k] = s.qvel[k]; p[W_MID_WARM + k] = s.warm[k]; }
+  for (int k = tid; k < m->nu; k += NT) p[W_MID_CTRL + k] = s.ctrl[k];
+  if (tid == 0) p[W_MID_NWARN] = (double)s.nwarn;
+}
+
+/* one env-step of env e into LDS (s, o), or the substeps [sub_begin, sub_end) of it.  Returns
+   W_DONE (results staged for w_commit), W_BAIL (the compact tier overflowed: nothing was written)
+   or W_PAUSED (sub_end < frame_skip: the state after substep sub_end - 1 is in LDS for
+   w_store_mid).  sub_begin > 0 resumes from the mid-step state `mid`, skipping the controller. */
+#define W_BAIL 0
+#define W_DONE 1
+#define W_PAUSED 2
+template <int NT, class KS>
+WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
+                       const double* __restrict__ actions, int adim, KS& s, WOut& o, int sub_begin = 0,
+                       int sub_end = 1 << 30, const double* __restrict__ mid = nullptr) {
   const int tid = w_lane();
   WT_START();
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
   for (int k = tid; k < NCARRY; k += NT) o.carry[k] = st.carry[SC(st, k, e)];
   SYNC();
+  if (sub_begin > 0) {
+    /* resume: the state after the previous unit's substeps, and the ctrl it applied */
+    const double* p = mid + (size_t)e * W_MID;
+    for (int k = tid; k < m->nq; k += NT) s.qpos[k] = p[W_MID_QPOS + k];
+    for (int k = tid; k < m->nv; k += NT) { s.qvel[k] = p[W_MID_QVEL + k]; s.warm[k] = p[W_MID_WARM + k]; }
+    for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = p[W_MID_CTRL + k];
+    if (tid == 0) s.nwarn = (int)p[W_MID_NWARN];
+    SYNC();
+  }
   WT(24);
-  if (tid == 0) {
+  if (tid == 0 && sub_begin == 0) {
     double ctrl[K_NU];
     if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L || c.task == UR3E_TASK_GYM_V0 ||
         c.task == UR3E_TASK_IMIT_INDIRECT) {
@@ -972,7 +1008,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
   SYNC();
   const int fs = (k_is_gym(c.task) || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
   /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
-  int sub = 0, retried = 0, resetting = 0;
+  int sub = sub_begin, retried = 0, resetting = 0;
   w_step_pre<NT>(m, s);
   for (;;) {
     /* the model and plan are read-only kernel arguments, so their loads are invariant and LICM
@@ -991,10 +1027,10 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
 #define m mi
 #define pl pli
     w_forward<NT>(m, pl, s);
-    if (KS::BAIL && s.ovf) return false;
+    if (KS::BAIL && s.ovf) return W_BAIL;
     if (resetting) {
       w_reset_finish<NT>(m, pl, c, s, o);
-      return true;
+      return W_DONE;
     }
     if (!retried && w_step_badacc<NT>(m, s)) {
       retried = 1;
@@ -1003,6 +1039,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
     w_step_euler<NT>(m, pl, s);
     retried = 0;
     if (++sub < fs) {
+      if (sub >= sub_end) return W_PAUSED;
       w_step_pre<NT>(m, s);
       continue;
     }
@@ -1015,7 +1052,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
         if (c.obs_sites) w_obs_v2(m, s, o.obs);
       }
       SYNC();
-      return true;
+      return W_DONE;
     }
     if (tid == 0 && c.task != UR3E_TASK_GYM_V2) {
       /* ur3e-v0 / imitation envs: truncation tests t before the increment (ur3e_env.py:152-163,
@@ -1063,7 +1100,7 @@ WD bool w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c
       resetting = 1;
       continue;
     }
-    return true;
+    return W_DONE;
 #undef m
 #undef pl
   }
@@ -1123,7 +1160,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   WT_INIT();
-  if (!w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o)) {
+  if (w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
     if (threadIdx.x == 0) {
       /* each env is appended at most once per step and the fallback kernel re-zeroes the counter,
          so the slot is < n; the bound check keeps a corrupted counter from writing out of range */
@@ -1146,6 +1183,109 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
                             ((unsigned long long)blockIdx.x << 32);
   }
 #endif
+}
+
+/* Queued compact-tier step (gym tasks, frame_skip > 1): a resident pool of workgroups pulls
+   (substep, env) units from one device counter -- all envs' substep 0 first, then substep 1, ...
+   A unit of substep k > 0 waits for env e's unit k - 1 (flag[e], released after its mid-step state
+   is in HBM), resumes from that state, and the last substep runs the epilogue and commits.  Work is
+   balanced at substep granularity, so the launch ends about half an env-step after the average
+   instead of a whole slow env-step after it (a 4,096-env launch runs 2,048 envs at a time).
+   Results are identical to w_env_step: every env runs the same substeps in the same order.
+   qctl = {next unit, workgroups done, epoch}: the last workgroup to finish re-zeroes the counters
+   and advances the epoch, so the flags of this launch (epoch << 4 | substeps done, or
+   epoch << 4 | 15 once the env bailed to the full-capacity tier) never match a later launch's.
+   A producer unit was pulled before its consumer by a running workgroup and always releases its
+   flag (done or bailed), so every wait ends; the spin is bounded anyway, and a consumer that gives
+   up claims the env for the full-capacity tier instead (atomic exchange: exactly one appender). */
+#define W_FLAG_BAILED 15
+#define W_SPIN_LIMIT (1u << 26)
+KD int w_flag_acquire(const int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+
+template <int NT, class KS>
+__global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_model_t* __restrict__ m,
+                                                                  const KPlan* __restrict__ pl, KConfig c, KState st,
+                                                                  const double* __restrict__ actions, int adim,
+                                                                  double* __restrict__ obs_out,
+                                                                  double* __restrict__ rew_out,
+                                                                  unsigned char* __restrict__ term_out,
+                                                                  unsigned char* __restrict__ trunc_out,
+                                                                  double* __restrict__ tobs_out, int* __restrict__ ovf_list,
+                                                                  int* ovf_ctl, int* qctl, int* flags,
+                                                                  double* __restrict__ mid) {
+  __shared__ KS s;
+  __shared__ WOut o;
+  __shared__ int s_u, s_epoch, s_flag;
+  const int tid = threadIdx.x;
+  const int n = st.n, fs = c.frame_skip, total = n * fs;
+  if (tid == 0) s_epoch = __hip_atomic_load(qctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  SYNC();
+  const int E = s_epoch;
+  const int bailed = (E << 4) | W_FLAG_BAILED;
+  for (;;) {
+    if (tid == 0) s_u = atomicAdd(qctl, 1);
+    SYNC();
+    const int u = s_u;
+    if (u >= total) break;
+    const int sub = u / n;
+    const int e = k_xcd_env(u - sub * n, n);
+    if (sub > 0) {
+      if (tid == 0) {
+        const int want = (E << 4) | sub;
+        int f = w_flag_acquire(flags + e);
+        unsigned int spins = 0;
+        while (f != want && f != bailed) {
+          if (++spins > W_SPIN_LIMIT) {
+            const int old = atomicExch(flags + e, bailed);
+            if (old == want) {
+              f = want; /* released while we gave up: keep going (and keep the flag final) */
+              atomicExch(flags + e, want);
+            } else {
+              f = bailed;
+              if (old != bailed) ovf_list[min(atomicAdd(ovf_ctl, 1), n - 1)] = e;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          f = w_flag_acquire(flags + e);
+        }
+        s_flag = f;
+      }
+      SYNC();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (s_flag == bailed) continue;
+    }
+    const int r = w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o, sub, sub + 1, mid);
+    if (r == W_BAIL) {
+      if (tid == 0) {
+        /* the full-capacity tier recomputes the whole env-step from the committed state */
+        const int old = sub + 1 < fs ? atomicExch(flags + e, bailed) : 0;
+        if (old != bailed) {
+          const int slot = atomicAdd(ovf_ctl, 1);
+          if (slot < n) ovf_list[slot] = e;
+        }
+      }
+    } else if (r == W_PAUSED) {
+      w_store_mid<NT>(m, mid, e, s);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      SYNC();
+      if (tid == 0) {
+        const int old = atomicExch(flags + e, (E << 4) | (sub + 1));
+        if (old == bailed) atomicExch(flags + e, bailed); /* a consumer gave up and claimed the env */
+      }
+    } else {
+      w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+    }
+    SYNC();
+  }
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(qctl + 1, 1) == (int)gridDim.x - 1) {
+      atomicExch(qctl, 0);
+      atomicExch(qctl + 1, 0);
+      atomicExch(qctl + 2, (E + 1) & 0x7ffffff);
+    }
+  }
 }
 
 /* full-capacity tier over the envs the compact tier queued (grid-stride over the list).
@@ -1266,6 +1406,11 @@ struct ur3e_batch {
   int* d_ovf_list;
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
   unsigned long long* d_ovf_total;
+  int queued;      /* compact tier through the substep work queue (w_env_step_q) */
+  int q_grid;      /* resident workgroups of w_env_step_q (occupancy x CUs) */
+  int* d_qctl;     /* {next unit, workgroups done, epoch} */
+  int* d_flags;    /* [n] per-env substep hand-off flags */
+  double* d_mid;   /* [n][W_MID] mid-step state */
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
@@ -1468,6 +1613,25 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMalloc(&b->d_ovf_ctl, 2 * sizeof(int)));
   HIPCHK(hipMalloc(&b->d_ovf_total, sizeof(unsigned long long)));
   HIPCHK(hipMemset(b->d_ovf_ctl, 0, 2 * sizeof(int)));
+  /* substep work queue: gym tasks with several substeps per env-step on main.xml's compact tier
+     (cfg->schedule 1 keeps one workgroup per env-step) */
+  b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 && cfg->schedule != 1;
+  b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->q_grid = 0;
+  if (b->queued) {
+    int per_cu = 0, cus = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)w_env_step_q<64, KSS_NV>, 64, 0));
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    b->q_grid = per_cu * cus;
+    if (b->q_grid < 1) b->q_grid = 1;
+    const int units = n_envs * c.frame_skip;
+    if (b->q_grid > units) b->q_grid = units;
+    int qinit[3] = {0, 0, 1};
+    HIPCHK(hipMalloc(&b->d_qctl, 3 * sizeof(int)));
+    HIPCHK(hipMemcpy(b->d_qctl, qinit, sizeof(qinit), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&b->d_flags, sizeof(int) * nd));
+    HIPCHK(hipMemset(b->d_flags, 0, sizeof(int) * nd));
+    HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
+  }
   HIPCHK(hipMemset(b->d_ovf_total, 0, sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
@@ -1487,6 +1651,9 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   if (b->st.sensordata) (void)hipFree(b->st.sensordata);
+  if (b->d_qctl) (void)hipFree(b->d_qctl);
+  if (b->d_flags) (void)hipFree(b->d_flags);
+  if (b->d_mid) (void)hipFree(b->d_mid);
   (void)hipEventDestroy(b->ev0);
   (void)hipEventDestroy(b->ev1);
   delete b;
@@ -1530,7 +1697,11 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   }
   if (record) HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
-    if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
+    if (b->queued) /* substep work queue (w_env_step_q) */
+      hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid);
+    else if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
                          b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_ctl);
@@ -1662,7 +1833,8 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
   int nt;
   if (b->tiered) {
     nt = 64;
-    fn = b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
+    fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
+                   : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
   } else if (b->wave_nt == 128) {
     nt = 128;
     fn = (const void*)w_env_step<128, KSL>;

@@ -48,7 +48,7 @@ class ConfigC(ctypes.Structure):
         ("task_gains", ctypes.c_double * 12), ("joint_gains", ctypes.c_double * 12),
         ("seed", ctypes.c_ulonglong), ("env_id_offset", ctypes.c_int), ("envs_per_block", ctypes.c_int),
         ("tier_con_cap", ctypes.c_int), ("rot_joint_gains", ctypes.c_double * 12),
-        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int),
+        ("np_chunk_lanes", ctypes.c_int), ("sensors", ctypes.c_int), ("schedule", ctypes.c_int),
     ]
 
 
@@ -97,7 +97,7 @@ def load_model(name: str = "main"):
 def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
                 reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
                 task_gains=None, joint_gains=None, tier_con_cap=0, rot_joint_gains=None,
-                np_chunk_lanes=0, sensors=False) -> ConfigC:
+                np_chunk_lanes=0, sensors=False, schedule=0) -> ConfigC:
     c = ConfigC()
     c.task = task
     c.frame_skip = frame_skip
@@ -125,6 +125,7 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.tier_con_cap = tier_con_cap
     c.np_chunk_lanes = np_chunk_lanes
     c.sensors = int(sensors)
+    c.schedule = int(schedule)
     return c
 
 
