@@ -98,10 +98,12 @@ typedef struct ur3e_config_t {
                             mj_rnePostConstraint; assets/main.xml:384-405) for ur3e_batch_get_sensordata.
                             The torque sensors need the full-capacity layout, so the handle runs the
                             full-capacity tier (envs_per_block 0 -> 128 lanes per env; > 0 rejected) */
-  int schedule;          /* two-tier step launch: 0 (default) = gym tasks with frame_skip > 1 on main.xml run
-                            as a substep work queue (a resident pool of workgroups pulls (substep, env)
-                            units, state handed between substeps through HBM: balances the launch at
-                            substep granularity); 1 = one workgroup per env-step.  Same results. */
+  int schedule;          /* two-tier step launch: 0 (default, auto) = gym tasks with frame_skip > 1 on
+                            main.xml with more envs than resident workgroup slots run as a substep work
+                            queue (a resident pool of workgroups pulls (substep, env) units, state handed
+                            between substeps through HBM: balances the launch at substep granularity),
+                            otherwise one workgroup per env-step; 1 = always one workgroup per env-step;
+                            2 = always the queue (when applicable).  Same results either way. */
 } ur3e_config_t;
 
 typedef struct ur3e_batch ur3e_batch_t;

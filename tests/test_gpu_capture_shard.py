@@ -43,14 +43,16 @@ def _eq(torch, x, y, what):
     assert torch.equal(x, y), f"{what}: max diff {(x.double() - y.double()).abs().max().item()}"
 
 
-def test_graph_capture_replay_bit_exact():
+@pytest.mark.parametrize("schedule", [0, 2])
+def test_graph_capture_replay_bit_exact(schedule):
+    """schedule 2 captures the substep work queue (its unit counters and epoch live on the device)"""
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model("main")
     n, K, R = 128, 3, 100
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=21, tier_con_cap=2,
-                         max_episode_steps=40)
+                         max_episode_steps=40, schedule=schedule)
     ge = rt.Batch(mc, cfg, n)
     gg = rt.Batch(mc, cfg, n)
     ob = po.OracleBatch(mc, po.config_from(cfg), n)
@@ -181,8 +183,9 @@ def test_sharded_envs_rccl_self_gather(env_id):
 
 @pytest.mark.parametrize("n,cap", [(777, 0), (4096, 0), (512, 3)])
 def test_substep_queue_matches_env_step_launch(n, cap):
-    """The default two-tier launch of a gym step with frame_skip 2 is the substep work queue
-    (w_env_step_q: (substep, env) units, state handed over through HBM between substeps).  It must
+    """The substep work queue (w_env_step_q: (substep, env) units, state handed over through HBM
+    between substeps; the default launch above the resident slot count, forced here by schedule 2)
+    must
     equal the one-workgroup-per-env-step launch (schedule 1) bit for bit, every step, including
     envs that bail to the full-capacity tier in either substep (cap = diagnostic contact cap) and
     auto-resets; n = 777 is not a multiple of the 8 XCDs."""
@@ -190,7 +193,7 @@ def test_substep_queue_matches_env_step_launch(n, cap):
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model("main")
     kw = dict(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=17, max_episode_steps=40, tier_con_cap=cap)
-    gq = rt.Batch(mc, rt.make_config(schedule=0, **kw), n)
+    gq = rt.Batch(mc, rt.make_config(schedule=2, **kw), n)
     ge = rt.Batch(mc, rt.make_config(schedule=1, **kw), n)
     _eq(torch, gq.obs, ge.obs, "reset obs")
     rng = np.random.default_rng(8)
