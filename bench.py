@@ -416,7 +416,8 @@ def main():
             "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
                        "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (20 KB lifetime-overlaid LDS working set, 256 VGPRs: 8 envs/CU, 2 per SIMD)"
-                                            " + full-capacity fallback", -128: "full-capacity, 128 lanes per env",
+                                            " + full-capacity fallback; above the resident slot count the compact tier runs as a"
+                                            " substep work queue", -128: "full-capacity, 128 lanes per env",
                                             -64: "full-capacity, 64 lanes per env"}.get(
                            batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),
                        "kernel_resources": batch_kinfo,
@@ -430,7 +431,7 @@ def main():
                                        "note": "rank-0 stream time of the first env-steps after reset"}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic,
-                         "kernel": "w_env_step<64,KSS_NV> (+ w_env_step_list<128> fallback)",
+                         "kernel": batch_kinfo["kernel"] + " + w_env_step_list<128> fallback",
                          "kernel_ms": step_kernel_ms,
                          "stream_avg_ms": kernel_avg_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,

@@ -162,6 +162,10 @@ int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream);
 /* envs the compact tier handed to the full-capacity tier since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 
+/* the step kernel this handle launches: 0 compact tier, one workgroup per env-step; 1 compact tier
+   as a substep work queue; 2 full-capacity tier only; 3 one env per lane (v1) */
+int ur3e_batch_schedule(const ur3e_batch_t* b);
+
 /* observation width of the handle's task (24 or 13) */
 int ur3e_batch_obs_dim(const ur3e_batch_t* b);
 

@@ -1928,6 +1928,14 @@ extern "C" int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* to
 
 extern "C" int ur3e_batch_obs_dim(const ur3e_batch_t* b) { return b ? k_obs_dim(b->cfg.task) : 0; }
 
+/* which step kernel the handle launches: 0 compact tier, one workgroup per env-step (w_env_step);
+   1 compact tier as a substep work queue (w_env_step_q); 2 full-capacity tier only; 3 lane per env */
+extern "C" int ur3e_batch_schedule(const ur3e_batch_t* b) {
+  if (!b) return -1;
+  if (b->tiered) return b->queued ? 1 : 0;
+  return b->wave_nt ? 2 : 3;
+}
+
 extern "C" int ur3e_batch_num_envs(const ur3e_batch_t* b) { return b ? b->n : 0; }
 extern "C" int ur3e_batch_nq(const ur3e_batch_t* b) { return b ? b->host_model.nq : 0; }
 extern "C" int ur3e_batch_nv(const ur3e_batch_t* b) { return b ? b->host_model.nv : 0; }

@@ -76,7 +76,8 @@ def load_library():
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_sensordata.argtypes = [vp, vp, vp]
-    for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim"):
+    for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim",
+              "ur3e_batch_schedule"):
         getattr(L, f).argtypes = [vp]
     _lib = L
     del dp
@@ -263,11 +264,16 @@ class Batch:
         _check(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
         return int(v.value)
 
+    SCHEDULES = {0: "w_env_step<64,KSS_NV> (compact tier, one workgroup per env-step)",
+                 1: "w_env_step_q<64,KSS_NV> (compact tier, substep work queue)",
+                 2: "w_env_step<128|64,KSL> (full-capacity tier)", 3: "k_env_step (one env per lane)"}
+
     def kernel_info(self) -> dict:
-        """{envs_per_cu, lds_bytes, regs} of the step kernel this handle launches"""
+        """{envs_per_cu, lds_bytes, regs, kernel} of the step kernel this handle launches"""
         e, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
-        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value}
+        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value,
+                "kernel": self.SCHEDULES.get(self.L.ur3e_batch_schedule(self.h), "?")}
 
     def set_timing(self, on: bool = True):
         """Record HIP events around every (uncaptured) step, for last_step_ms()."""
