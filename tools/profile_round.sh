@@ -16,4 +16,5 @@ done
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $D/pmc_sq -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $D/pmc_sq.log 2>&1 || exit $?
 # lane utilisation (thread-cycles per VALU cycle) and the FP64 instruction mix
 timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_WAVES --output-format csv -d $D/pmc_sq2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $D/pmc_sq2.log 2>&1 || exit $?
-find $D -name "*.csv" | head -20
+python3 tools/filter_csv.py $D/trace/run_kernel_trace.csv $D/pmc_*/run_counter_collection.csv
+du -sh $D

@@ -943,10 +943,29 @@ template <int NT, class KS>
 WD void w_store_mid(KModel m, double* __restrict__ mid, int e, const KS& s) {
   const int tid = w_lane();
   double* p = mid + (size_t)e * W_MID;
-  for (int k = tid; k < m->nq; k += NT) w_put_sc1(p + W_MID_QPOS + k, s.qpos[k]);
-  for (int k = tid; k < m->nv; k += NT) { w_put_sc1(p + W_MID_QVEL + k, s.qvel[k]); w_put_sc1(p + W_MID_WARM + k, s.warm[k]); }
-  for (int k = tid; k < m->nu; k += NT) w_put_sc1(p + W_MID_CTRL + k, s.ctrl[k]);
-  if (tid == 0) w_put_sc1(p + W_MID_NWARN, (double)s.nwarn);
+  /* one 16-byte write-through store per lane (pairs of doubles): narrow sc1 stores each cost a
+     separate partial-line write */
+  if (tid < W_MID / 2) {
+    double v[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = 2 * tid + h;
+      double x = 0.0;
+      if (k < W_MID_QVEL) x = k < m->nq ? s.qpos[k] : 0.0;
+      else if (k < W_MID_WARM) x = k - W_MID_QVEL < m->nv ? s.qvel[k - W_MID_QVEL] : 0.0;
+      else if (k < W_MID_CTRL) x = k - W_MID_WARM < m->nv ? s.warm[k - W_MID_WARM] : 0.0;
+      else if (k < W_MID_NWARN) x = k - W_MID_CTRL < m->nu ? s.ctrl[k - W_MID_CTRL] : 0.0;
+      else if (k == W_MID_NWARN) x = (double)s.nwarn;
+      v[h] = x;
+    }
+    /* buffer descriptor over this env's mid record (wave-uniform base), aux 16 = sc1 */
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, W_MID * 8, 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+    const unsigned long long a = __builtin_bit_cast(unsigned long long, v[0]);
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v[1]);
+    u32x4_t w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc, 16 * tid, 0, 16);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* every storing lane drained before the flag */
 }
 
@@ -1242,12 +1261,14 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
   const int total = nper * fs;
   if (tid == 0) s_epoch = __hip_atomic_load(qctl + W_NQUEUE + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   SYNC();
-  const int E = s_epoch;
+  /* wave-uniform values read from LDS pass through readfirstlane so they live in SGPRs: kept in
+     VGPRs across the step they would be spilled (the kernel is at its 256-register budget) */
+  const int E = __builtin_amdgcn_readfirstlane(s_epoch);
   const int bailed = (E << 4) | W_FLAG_BAILED;
   for (;;) {
     if (tid == 0) s_u = atomicAdd(qctl + q, 1);
     SYNC();
-    const int u = s_u;
+    const int u = __builtin_amdgcn_readfirstlane(s_u);
     if (u >= total) break;
     const int sub = u / nper;
     const int e = q * nper + (u - sub * nper);
@@ -1275,7 +1296,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       }
       SYNC();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* payload loads are sc1: keep them below */
-      if (s_flag == bailed) continue;
+      if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
     const int r = w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o, sub, sub + 1, mid);
     if (r == W_BAIL) {
