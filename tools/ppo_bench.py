@@ -39,7 +39,7 @@ def main():
         group = dist.group.WORLD
     n = a.envs_per_gpu
     venv = UR3eVecEnv(num_envs=n, device=local, seed=0, env_id_offset=rank * n)
-    env = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10.0)
+    env = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10.0, group=group)
     algo = PPO(env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, device=f"cuda:{local}",
                seed=rank, group=group)
     algo.learn(1)  # warm-up: allocations, first kernels

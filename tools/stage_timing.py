@@ -20,7 +20,7 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 md, mc = rt.load_model("main")
-b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1, envs_per_block=epb), n)
+b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1, envs_per_block=epb, schedule=1), n)  # schedule 1: per-env-step kernel (the one with stage marks)
 L = rt.load_library()
 cyc = (ctypes.c_ulonglong * 32)(); calls = (ctypes.c_ulonglong * 32)()
 lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")

@@ -8,6 +8,13 @@ match SB3 (stable_baselines3==2.7.0) bit-for-bit on the same inputs.  `step_torc
 normalised float32 observations to a torch-ROCm policy without a host copy; `step_wait` keeps the
 SB3 VecEnv contract (numpy obs, rewards, dones, infos with the normalised terminal observation).
 
+Several ranks (one process per GPU, each stepping its own env shard): pass the
+process group.  SB3 keeps ONE RunningMeanStd over all envs of the VecEnv, so each step every rank
+all-gathers the shard outputs (one collective, rank-major = global env-id order) and runs the same
+statistics kernel over the whole global batch: the statistics, the per-env discounted returns and the
+normalised outputs are then identical on every rank and identical to a single-process VecNormalize over
+all envs; each rank keeps its own rows.
+
 Persistence: `save(path)` / `VecNormalize.load(path, venv)` write the statistics and settings to an
 .npz (SB3 pickles the wrapper object; its fields are the same).
 """
@@ -60,11 +67,20 @@ class _RMSView:
 
 class VecNormalize:
     def __init__(self, venv, training: bool = True, norm_obs: bool = True, norm_reward: bool = True,
-                 clip_obs: float = 10.0, clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8):
+                 clip_obs: float = 10.0, clip_reward: float = 10.0, gamma: float = 0.99, epsilon: float = 1e-8,
+                 group=None):
         import torch
         self.torch = torch
         self.venv = venv
         self.num_envs = venv.num_envs
+        # statistics run over every rank's envs (global env-id order); this rank owns rows [lo, lo + n)
+        self.group = group
+        if group is not None:
+            import torch.distributed as dist
+            self._world, self._rank = dist.get_world_size(group), dist.get_rank(group)
+        else:
+            self._world, self._rank = 1, 0
+        self.n_stats = self.num_envs * self._world
         self.observation_space = venv.observation_space
         self.action_space = venv.action_space
         self.render_mode = getattr(venv, "render_mode", None)
@@ -81,14 +97,18 @@ class VecNormalize:
         self._ret_mean = torch.zeros(1, **f64)
         self._ret_var = torch.ones(1, **f64)
         self._ret_count = torch.full((1,), 1e-4, **f64)
-        self._returns = torch.zeros(self.num_envs, **f64)
+        self._returns = torch.zeros(self.n_stats, **f64)
         self._st = StatsC(*[t.data_ptr() for t in (self._obs_mean, self._obs_var, self._obs_count, self._ret_mean,
                                                      self._ret_var, self._ret_count, self._returns)])
         self.training, self.norm_obs, self.norm_reward = training, norm_obs, norm_reward
         self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
-        self._obs_out = torch.empty((self.num_envs, dim), dtype=torch.float32, device=dev)
-        self._tobs_out = torch.zeros((self.num_envs, dim), dtype=torch.float32, device=dev)
-        self._rew_out = torch.empty(self.num_envs, **f64)
+        self._obs_out = torch.empty((self.n_stats, dim), dtype=torch.float32, device=dev)
+        self._tobs_out = torch.zeros((self.n_stats, dim), dtype=torch.float32, device=dev)
+        self._rew_out = torch.empty(self.n_stats, **f64)
+        if self._world > 1:
+            # one packed row per env: obs | terminal obs | reward | terminated | truncated
+            self._pack = torch.empty((self.num_envs, 2 * dim + 3), **f64)
+            self._gpack = torch.empty((self.n_stats, 2 * dim + 3), **f64)
         self.old_obs = None
         self.old_reward = None
         self._actions = None
@@ -104,7 +124,7 @@ class VecNormalize:
 
     @property
     def returns(self):
-        return self._returns.cpu().numpy().copy()
+        return self._mine(self._returns).cpu().numpy().copy()
 
     def _cfg(self):
         return CfgC(int(self.training), int(self.norm_obs), int(self.norm_reward), float(self.clip_obs),
@@ -114,28 +134,60 @@ class VecNormalize:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     # -- device path ---------------------------------------------------------
-    def reset_torch(self):
-        obs = self.venv.stepper.reset()
-        self.old_obs = obs
-        rt._check(self.L.ur3e_vecnorm_reset(ctypes.byref(self._st), ctypes.byref(self._cfg()), self.num_envs,
-                                            self.dim, ctypes.c_void_p(obs.data_ptr()),
-                                            ctypes.c_void_p(self._obs_out.data_ptr()), self._stream()))
-        return self._obs_out if self.norm_obs else obs
+    def _kernel_reset(self, n, obs, obs_out):
+        rt._check(self.L.ur3e_vecnorm_reset(ctypes.byref(self._st), ctypes.byref(self._cfg()), n, self.dim,
+                                            ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(obs_out.data_ptr()),
+                                            self._stream()))
 
-    def step_torch(self, actions):
-        """(normalised obs f32, normalised reward, terminated, truncated, normalised terminal obs f32)
-        as device tensors; raw step outputs stay in old_obs / old_reward."""
-        obs, rew, term, trunc, tobs = self.venv.step_torch(actions)
-        self.old_obs, self.old_reward = obs, rew
-        self._last = (term, trunc, tobs)
-        rt._check(self.L.ur3e_vecnorm_step(ctypes.byref(self._st), ctypes.byref(self._cfg()), self.num_envs, self.dim,
+    def _kernel_step(self, n, obs, rew, term, trunc, tobs):
+        rt._check(self.L.ur3e_vecnorm_step(ctypes.byref(self._st), ctypes.byref(self._cfg()), n, self.dim,
                                            *[ctypes.c_void_p(t.data_ptr()) for t in (obs, rew, term, trunc, tobs,
                                                                                     self._obs_out, self._rew_out,
                                                                                     self._tobs_out)],
                                            self._stream()))
-        o = self._obs_out if self.norm_obs else obs
-        to = self._tobs_out if self.norm_obs else tobs
-        return o, self._rew_out, term, trunc, to
+
+    def _gather(self, obs, tobs=None, rew=None, term=None, trunc=None):
+        """All ranks' shard outputs in global env-id order (one all-gather of packed rows)."""
+        import torch.distributed as dist
+        d = self.dim
+        p = self._pack
+        p[:, :d].copy_(obs)
+        if tobs is not None:
+            p[:, d:2 * d].copy_(tobs)
+            p[:, 2 * d].copy_(rew)
+            p[:, 2 * d + 1].copy_(term)
+            p[:, 2 * d + 2].copy_(trunc)
+        dist.all_gather_into_tensor(self._gpack, p, group=self.group)
+        g = self._gpack
+        u8 = self.torch.uint8
+        return (g[:, :d].contiguous(), g[:, d:2 * d].contiguous(), g[:, 2 * d].contiguous(),
+                g[:, 2 * d + 1].to(u8), g[:, 2 * d + 2].to(u8))
+
+    def _mine(self, t):
+        lo = self._rank * self.num_envs
+        return t[lo:lo + self.num_envs]
+
+    def reset_torch(self):
+        obs = self.venv.stepper.reset()
+        self.old_obs = obs
+        gobs = self._gather(obs)[0] if self._world > 1 else obs
+        self._kernel_reset(self.n_stats, gobs, self._obs_out)
+        return self._mine(self._obs_out) if self.norm_obs else obs
+
+    def step_torch(self, actions):
+        """(normalised obs f32, normalised reward, terminated, truncated, normalised terminal obs f32)
+        as device tensors for this rank's envs; raw step outputs stay in old_obs / old_reward."""
+        obs, rew, term, trunc, tobs = self.venv.step_torch(actions)
+        self.old_obs, self.old_reward = obs, rew
+        self._last = (term, trunc, tobs)
+        if self._world > 1:
+            gobs, gtobs, grew, gterm, gtrunc = self._gather(obs, tobs, rew, term, trunc)
+            self._kernel_step(self.n_stats, gobs, grew, gterm, gtrunc, gtobs)
+        else:
+            self._kernel_step(self.n_stats, obs, rew, term, trunc, tobs)
+        o = self._mine(self._obs_out) if self.norm_obs else obs
+        to = self._mine(self._tobs_out) if self.norm_obs else tobs
+        return o, self._mine(self._rew_out), term, trunc, to
 
     def normalize_obs_torch(self, obs):
         obs = obs.to(device=self.device, dtype=self.torch.float64).contiguous()
