@@ -179,7 +179,7 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
     for t in range(g0):
         drv.batch.step(drv.traj.row(t))
     rows = [drv.traj.row(t) for t in range(g0, g1)]
-    ovf0 = drv.batch.overflow_count()
+    tc0 = drv.batch.tier_counts()
     it = iter(rows)
     steps_c3 = g1 - g0
     torch.cuda.synchronize()
@@ -189,10 +189,14 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
         drv.batch.step(next(it))
     e1.record()
     torch.cuda.synchronize()
-    fb = drv.batch.overflow_count() - ovf0
+    tc = [x - y for x, y in zip(drv.batch.tier_counts(), tc0)]
+    tot = float(n_envs * steps_c3)
     out["C3_main_move_l_mug"] = {"value": n_envs * steps_c3 / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s",
                                  "envs": n_envs, "substeps_per_env_step": 1, "rows": [g0, g1],
-                                 "fallback_env_steps_frac": fb / float(n_envs * steps_c3)}
+                                 # env-steps beyond the compact tier's capacity: routed to the grasp tier by
+                                 # the previous step's contact count, or handed on mid-step (and beyond it)
+                                 "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot,
+                                 "full_tier_frac": tc[1] / tot}
     drv.close()
     return out
 

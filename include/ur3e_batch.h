@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 4
+#define UR3E_ABI_VERSION 5
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -82,15 +82,19 @@ typedef struct ur3e_config_t {
   unsigned long long seed; /* Philox key for reset noise */
   int env_id_offset;     /* global id of local env 0 (multi-GPU shards) */
   int envs_per_block;    /* kernel layout:
-                            0 (default) = two-tier: one 64-lane wavefront per env with a compact
+                            0 (default) = tiered: one 64-lane wavefront per env with a compact
                               LDS working set (<= W_SMALL_MAXCON contacts / W_SMALL_MAXEFC rows,
-                              four envs per CU); an env that exceeds it in any substep is
-                              recomputed, same step, by the full-capacity tier;
+                              eight envs per CU); an env that exceeds it in any substep is
+                              recomputed, same step, by the grasp tier (main.xml: the same code
+                              path sized for W_GRASP_MAXCON contacts / W_GRASP_MAXEFC rows), and
+                              one that exceeds that by the full-capacity tier;
                             -128 = full-capacity tier only, 128-lane workgroup per env;
                             -64 = full-capacity tier only, 64-lane wavefront per env;
                             1..64 = one env per lane, that many envs per wavefront (v1) */
-  int tier_con_cap;      /* diagnostic (0 = off): the compact tier treats more than this many
-                            contacts as overflow, to exercise the fallback path */
+  int tier_con_cap;      /* diagnostic (0 = off): > 0: the compact tier treats more than this many
+                            contacts as overflow (its envs run in the grasp tier); < 0: the compact
+                            and the grasp tier both treat more than -tier_con_cap contacts as
+                            overflow (the envs reach the full-capacity tier) */
   double rot_joint_gains[12]; /* kp[6], kd[6] of the rotation PD in move_l (config_l.yml "rot") */
   int np_chunk_lanes;    /* diagnostic (0 = 16): survivor lanes per compact-tier narrowphase chunk;
                             smaller values exercise its multi-chunk path */
@@ -159,8 +163,14 @@ int ur3e_batch_get_sensordata(ur3e_batch_t* b, double* d_sensordata, void* strea
    `u` that gymnasium_src/scripts/imitation_rl/collect_demos.py:134-148 records as the direct action */
 int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream);
 
-/* envs the compact tier handed to the full-capacity tier since create (synchronises) */
+/* env-steps the compact tier handed on to the fallback tiers since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
+
+/* since create (synchronises): counts[0] env-steps the compact tier handed on to the grasp tier,
+   counts[1] env-steps the grasp tier handed on to the full-capacity tier, counts[2] env-steps routed
+   straight to the grasp tier (the env's previous forward had more than 8 contacts; it runs on an
+   internal stream concurrently with the compact tier) */
+int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
 
 /* the step kernel this handle launches: 0 compact tier, one workgroup per env-step; 1 compact tier
    as a substep work queue; 2 full-capacity tier only; 3 one env per lane (v1) */

@@ -214,3 +214,55 @@ def test_substep_queue_matches_env_step_launch(n, cap):
         assert oq > 0 and oe > 0
     gq.close()
     ge.close()
+
+
+def test_graph_capture_grasp_routing():
+    """The tier routing inside a captured step: the scripted pick (C3 semantics) in its grasp rows,
+    where envs hold 12-20 contacts, so each step routes them to the grasp tier on the library's
+    internal stream (fork/join events inside the graph) while the compact tier skips them.  A
+    3-step graph replayed 60 times over rows 1850..2030 must equal the same rows stepped eagerly and
+    the oracle, with routed env-steps counted inside the replays."""
+    torch = _torch()
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    n, K, R, r0 = 32, 3, 60, 1850
+    de = MoveLMug(n, reset_mode="low", seed=5)
+    dg = MoveLMug(n, reset_mode="low", seed=5)
+    ob = po.OracleBatch(de.batch.model_c, po.config_from(de.batch.cfg), n)
+    for t in range(r0):
+        row = de.traj.row(t)
+        de.batch.step(row)
+        dg.batch.step(row)
+        ob.step(row.cpu().numpy())
+    dev = de.batch.obs.device
+    static_a = torch.zeros((K, n, 7), dtype=torch.float64, device=dev)
+    graph = torch.cuda.CUDAGraph()
+    snaps = []
+    with torch.cuda.graph(graph):
+        for k in range(K):
+            out = dg.batch.step(static_a[k])
+            snaps.append(out[0].clone())
+    routed0 = dg.batch.tier_counts()[2]
+    t = r0
+    for r in range(R):
+        rows = torch.stack([de.traj.row(t + k) for k in range(K)])
+        static_a.copy_(rows)
+        graph.replay()
+        for k in range(K):
+            e_obs = de.batch.step(rows[k])[0]
+            o_obs = ob.step(rows[k].cpu().numpy())[0]
+            _eq(torch, snaps[k], e_obs, f"obs replay {r} step {k}")
+            np.testing.assert_array_equal(snaps[k].cpu().numpy(), o_obs, err_msg=f"obs vs oracle replay {r} step {k}")
+        t += K
+        for x, y, what in zip(dg.batch.get_state(), de.batch.get_state(), ("qpos", "qvel", "warmstart")):
+            _eq(torch, x, y, f"{what} after replay {r}")
+    torch.cuda.synchronize()
+    oqp, oqv, owa, onc = ob.get_state()
+    qp, qv, wa = dg.batch.get_state()
+    np.testing.assert_array_equal(qp.cpu().numpy(), oqp)
+    np.testing.assert_array_equal(qv.cpu().numpy(), oqv)
+    np.testing.assert_array_equal(dg.batch.get_info()["ncon"].cpu().numpy(), onc)
+    assert dg.batch.tier_counts()[2] > routed0  # envs were routed to the grasp tier inside the replays
+    assert int(onc.max()) > 10  # the grasp exceeded the compact tier's contact capacity
+    de.close()
+    dg.close()

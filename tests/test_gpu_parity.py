@@ -74,6 +74,7 @@ def _run_pair(model_name, task, n, steps, action_fn, frame_skip=2, seed=7, epb=0
                 max_touch[0] = max(max_touch[0], float(ot.max()))
     assert max_dq <= 1e-5
     gb.ovf = gb.overflow_count()
+    gb.tiers = gb.tier_counts()
     gb.n_done = n_done
     gb.max_touch = max_touch[0]
     gb.close()
@@ -124,14 +125,19 @@ def test_narrowphase_chunks(lanes):
     _run_pair("main", 0, 64, 100, _grasp_actions, seed=3, np_chunk_lanes=lanes)
 
 
-@pytest.mark.parametrize("cap", [2, 3])
+@pytest.mark.parametrize("cap", [2, 3, -2])
 def test_two_tier_fallback(cap):
     """Compact-tier overflow mid-step (the diagnostic cap makes envs with more than `cap` contacts
-    overflow in either substep or in an auto-reset) hands the env to the full-capacity tier, which
-    recomputes the step from the untouched state: results stay bit-exact, the fallback is taken,
-    including mid-step bails after a substep already ran."""
+    overflow in either substep or in an auto-reset) hands the env to the grasp tier (cap > 0) or,
+    when the grasp tier is capped too (cap < 0), on to the full-capacity tier; each recomputes the
+    step from the untouched state: results stay bit-exact, the fallback is taken, including
+    mid-step bails after a substep already ran."""
     gb = _run_pair("main", 0, 64, 80, _grasp_actions, seed=11, tier_con_cap=cap)
-    assert gb.ovf > 0
+    assert gb.ovf > 0 and gb.tiers[0] == gb.ovf
+    if cap > 0:
+        assert gb.tiers[1] == 0  # the grasp tier held every env the compact tier handed on
+    else:
+        assert gb.tiers[1] > 0  # ... and with it capped the envs reached the full-capacity tier
 
 
 def test_move_j_2f85():
@@ -267,6 +273,10 @@ def test_move_l_mug_scripted_pick():
             grasped |= o_obs[:, 23] == 1.0
     assert grasped.sum() >= n // 4
     assert (gb.obs[:, 5].cpu().numpy() - z0).max() > 0.01
+    # the firm grasp exceeds the compact tier (12-20 contacts): those env-steps ran in the grasp tier,
+    # handed on by the compact tier or routed there by the previous step's contact count
+    tc = gb.tier_counts()
+    assert tc[0] + tc[2] > 0 and tc[2] > 0, tc
     st = task_space_state(gb)
     assert st.shape == (n, 7)
     drv.close()

@@ -14,7 +14,8 @@ VARIANTS = {
     "two_tier_per_env_step": dict(schedule=1),
     "full_tier_128": dict(envs_per_block=-128),
     "full_tier_64": dict(envs_per_block=-64),
-    "forced_fallback_cap3": dict(tier_con_cap=3),
+    "grasp_tier_cap3": dict(tier_con_cap=3),
+    "full_tier_chain_cap-3": dict(tier_con_cap=-3),
 }
 
 

@@ -385,7 +385,15 @@ struct KState {
   double* touch; /* [env][UR3E_MAXTOUCH] touch sensors after the last forward */
   double* ctrl;  /* [env][UR3E_MAXU] d.ctrl after the last step (the controller output it applied) */
   double* sensordata; /* [env][UR3E_MAXSENSORDATA] mjData.sensordata of the last forward (sensors on) */
+  /* tier routing (grasp tier on): hint[e] = the env's last committed forward had more than
+     W_ROUTE_NCON contacts; route[e] = the snapshot of hint the current step routes by (written only
+     between steps, by the last kernel of the step): routed envs skip the compact tier and run in the
+     grasp tier concurrently with it.  Routing only picks the tier; every tier gives the same result. */
+  unsigned char* hint;
+  unsigned char* route;
 };
+/* an env whose last forward had more contacts than this runs its next step in the grasp tier */
+#define W_ROUTE_NCON 8
 
 struct KConfig {
   int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
@@ -832,7 +840,11 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
   if (tid == 0) {
     s.nwarn = st.nwarn[e];
     s.ovf = 0;
-    s.cap_con = (KS::BAIL && c.tier_con_cap > 0 && c.tier_con_cap < KS::MAXCON) ? c.tier_con_cap : KS::MAXCON;
+    /* diagnostic contact cap: > 0 caps the compact tier only (its envs then run in the grasp tier),
+       < 0 caps every bailing tier (compact and grasp: the envs reach the full-capacity tier) */
+    const int cap = c.tier_con_cap, capv = cap > 0 ? cap : -cap;
+    const bool capped = KS::BAIL && (cap < 0 || (cap > 0 && KS::MAXCON <= W_SMALL_MAXCON));
+    s.cap_con = (capped && capv < KS::MAXCON) ? capv : KS::MAXCON;
     if constexpr (KS::OVERLAY) s.np_lanes = c.np_lanes;
     else s.sens = c.sensors;
     o.t = st.t[e]; o.ep_len = st.ep_len[e]; o.ep_return = st.ep_return[e]; o.episode = st.episode[e];
@@ -858,6 +870,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   const int od = k_obs_dim(c.task);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
+    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > W_ROUTE_NCON);
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
     if (stepped && k_is_gym(c.task)) {
       if (rew_out) rew_out[e] = o.r;
@@ -1191,6 +1204,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
   __shared__ WOut o;
   if ((int)blockIdx.x >= st.n) return;
   const int e = k_xcd_env((int)blockIdx.x, st.n);
+  if (st.route && __builtin_amdgcn_readfirstlane(st.route[e])) return; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1272,6 +1286,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     if (u >= total) break;
     const int sub = u / nper;
     const int e = q * nper + (u - sub * nper);
+    if (st.route && __builtin_amdgcn_readfirstlane(st.route[e])) continue; /* stepped by the grasp tier */
     if (sub > 0) {
       if (tid == 0) {
         const int want = (E << 4) | sub;
@@ -1330,24 +1345,48 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
   }
 }
 
-/* full-capacity tier over the envs the compact tier queued (grid-stride over the list).
+/* a fallback tier over the envs the tier before it queued (grid-stride over the list): the grasp
+   tier (KSG_NV, 64 lanes) over the compact tier's list, the full-capacity tier (KSL, 128 lanes) over
+   the grasp tier's list.  Each recomputes the whole env-step from the committed state.  A bailing
+   tier (KS::BAIL) appends the envs it cannot hold to next_list for the tier after it.
    ovf_ctl = {count, blocks_done}: every workgroup reads the count, then the last workgroup to have
-   read it re-zeroes both, so the next step's compact kernel starts from an empty list.  The counter
-   lives and is reset entirely on the device, so a step captured into a HIP graph replays correctly
-   any number of times (no host-side step parity baked into the graph). */
-template <int NT>
-__global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __restrict__ m,
-                                                       const KPlan* __restrict__ pl, KConfig c, KState st,
-                                                       const double* __restrict__ actions, int adim,
-                                                       double* __restrict__ obs_out, double* __restrict__ rew_out,
-                                                       unsigned char* __restrict__ term_out,
-                                                       unsigned char* __restrict__ trunc_out,
-                                                       double* __restrict__ tobs_out,
-                                                       const int* __restrict__ ovf_list, int* ovf_ctl,
-                                                       unsigned long long* __restrict__ ovf_total) {
-  __shared__ KSL s;
+   read it re-zeroes both, so the next step's producer starts from an empty list.  The counters live
+   and are reset entirely on the device, so a step captured into a HIP graph replays correctly any
+   number of times (no host-side step parity baked into the graph). */
+template <int NT, class KS>
+__global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __restrict__ m,
+                                                          const KPlan* __restrict__ pl, KConfig c, KState st,
+                                                          const double* __restrict__ actions, int adim,
+                                                          double* __restrict__ obs_out, double* __restrict__ rew_out,
+                                                          unsigned char* __restrict__ term_out,
+                                                          unsigned char* __restrict__ trunc_out,
+                                                          double* __restrict__ tobs_out,
+                                                          const int* __restrict__ ovf_list, int* ovf_ctl,
+                                                          unsigned long long* __restrict__ ovf_total,
+                                                          int* __restrict__ next_list, int* next_ctl,
+                                                          int* __restrict__ pred_list, int* pred_ctl) {
+  __shared__ KS s;
   __shared__ WOut o;
   __shared__ int s_cnt;
+  if (pred_list && blockIdx.x == 0) {
+    /* the last kernel of the step: snapshot the routing hints for the next step and list the routed
+       envs for its grasp-tier pre-pass (the order of the list does not matter: envs are independent) */
+    if (threadIdx.x == 0) s_cnt = 0;
+    SYNC();
+    for (int e = threadIdx.x; e < st.n; e += NT) {
+      const unsigned char h = st.hint[e];
+      st.route[e] = h;
+      if (h) pred_list[atomicAdd(&s_cnt, 1)] = e;
+    }
+    SYNC();
+    if (threadIdx.x == 0) __hip_atomic_store(pred_ctl, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SYNC();
+  }
+  /* the producer launch has completed, so every workgroup reads the same final count: with an
+     empty list (the common case) there is nothing to reset and each workgroup leaves at once,
+     without the done-counter atomic (one contended atomic per workgroup costs ~10 us per launch) */
+  if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ovf_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+    return;
   if (threadIdx.x == 0) {
     int cnt = __hip_atomic_load(ovf_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cnt = cnt < st.n ? cnt : st.n;
@@ -1362,8 +1401,16 @@ __global__ __launch_bounds__(NT) void w_env_step_list(const ur3e_model_t* __rest
   const int cnt = s_cnt;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int e = ovf_list[i];
-    w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
-    w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+    if (w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
+      if constexpr (KS::BAIL) {
+        if (threadIdx.x == 0) {
+          const int slot = atomicAdd(next_ctl, 1);
+          if (slot < st.n) next_list[slot] = e;
+        }
+      }
+    } else {
+      w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+    }
     SYNC();
   }
 }
@@ -1447,7 +1494,15 @@ struct ur3e_batch {
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
   int* d_ovf_list;
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
-  unsigned long long* d_ovf_total;
+  unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier */
+  int grasp;       /* the tiers are compact -> grasp (KSG_NV) -> full capacity (main.xml only) */
+  int g_grid;      /* resident workgroups of the grasp-tier list kernel */
+  int* d_ovf2_list; /* envs the grasp tier handed to the full-capacity tier */
+  int* d_ovf2_ctl;
+  int* d_pred_list; /* envs routed to the grasp tier for the next step (route snapshot) */
+  int* d_pred_ctl;
+  hipStream_t side; /* the grasp-tier pre-pass runs here, concurrently with the compact tier */
+  hipEvent_t ev_fork, ev_join;
   int queued;      /* compact tier through the substep work queue (w_env_step_q) */
   int q_grid;      /* resident workgroups of w_env_step_q (occupancy x CUs) */
   int* d_qctl;     /* {next unit per queue [W_NQUEUE], workgroups done, epoch} */
@@ -1653,8 +1708,34 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_ctl, 2 * sizeof(int)));
-  HIPCHK(hipMalloc(&b->d_ovf_total, sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&b->d_ovf_total, 3 * sizeof(unsigned long long)));
   HIPCHK(hipMemset(b->d_ovf_ctl, 0, 2 * sizeof(int)));
+  /* grasp tier between the compact and the full-capacity tier (main.xml's specialised kernels) */
+  b->grasp = tiered && b->main_tree;
+  b->d_ovf2_list = nullptr; b->d_ovf2_ctl = nullptr; b->g_grid = 0;
+  b->d_pred_list = nullptr; b->d_pred_ctl = nullptr; b->side = nullptr;
+  s.hint = nullptr; s.route = nullptr;
+  if (b->grasp) {
+    int per_cu = 0, cus = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)w_env_step_list<64, KSG_NV>, 64, 0));
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    b->g_grid = per_cu * cus;
+    if (b->g_grid < 1) b->g_grid = 1;
+    if (b->g_grid > n_envs) b->g_grid = n_envs;
+    HIPCHK(hipMalloc(&b->d_ovf2_list, sizeof(int) * nd));
+    HIPCHK(hipMalloc(&b->d_ovf2_ctl, 2 * sizeof(int)));
+    HIPCHK(hipMemset(b->d_ovf2_ctl, 0, 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&b->d_pred_list, sizeof(int) * nd));
+    HIPCHK(hipMalloc(&b->d_pred_ctl, 2 * sizeof(int)));
+    HIPCHK(hipMemset(b->d_pred_ctl, 0, 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&s.hint, nd));
+    HIPCHK(hipMemset(s.hint, 0, nd));
+    HIPCHK(hipMalloc(&s.route, nd));
+    HIPCHK(hipMemset(s.route, 0, nd));
+    HIPCHK(hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+  }
   /* substep work queue: gym tasks with several substeps per env-step on main.xml's compact tier
      (cfg->schedule 1 keeps one workgroup per env-step) */
   b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 && cfg->schedule != 1;
@@ -1684,7 +1765,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMemset(b->d_flags, 0, sizeof(int) * nd));
     HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
   }
-  HIPCHK(hipMemset(b->d_ovf_total, 0, sizeof(unsigned long long)));
+  HIPCHK(hipMemset(b->d_ovf_total, 0, 3 * sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
   /* qpos0 / zero state; like a gymnasium Env, call ur3e_batch_reset before the first step */
@@ -1704,6 +1785,17 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   for (void* p : bufs) (void)hipFree(p);
   if (b->st.sensordata) (void)hipFree(b->st.sensordata);
   if (b->d_qctl) (void)hipFree(b->d_qctl);
+  if (b->d_ovf2_list) (void)hipFree(b->d_ovf2_list);
+  if (b->d_ovf2_ctl) (void)hipFree(b->d_ovf2_ctl);
+  if (b->d_pred_list) (void)hipFree(b->d_pred_list);
+  if (b->d_pred_ctl) (void)hipFree(b->d_pred_ctl);
+  if (b->st.hint) (void)hipFree(b->st.hint);
+  if (b->st.route) (void)hipFree(b->st.route);
+  if (b->side) {
+    (void)hipStreamDestroy(b->side);
+    (void)hipEventDestroy(b->ev_fork);
+    (void)hipEventDestroy(b->ev_join);
+  }
   if (b->d_flags) (void)hipFree(b->d_flags);
   if (b->d_mid) (void)hipFree(b->d_mid);
   (void)hipEventDestroy(b->ev0);
@@ -1749,6 +1841,17 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
   }
   if (record) HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
+    if (b->grasp) {
+      /* fork: envs routed by the last step's hints run in the grasp tier on the side stream while
+         the compact tier (which skips them) runs here */
+      HIPCHK(hipEventRecord(b->ev_fork, st));
+      HIPCHK(hipStreamWaitEvent(b->side, b->ev_fork, 0));
+      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(b->g_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
+                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_pred_list, b->d_pred_ctl, b->d_ovf_total + 2, b->d_ovf2_list, b->d_ovf2_ctl,
+                         nullptr, nullptr);
+      HIPCHK(hipEventRecord(b->ev_join, b->side));
+    }
     if (b->queued) /* substep work queue (w_env_step_q) */
       hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                          b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
@@ -1762,9 +1865,23 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
                          d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
                          b->d_ovf_ctl);
     int grid = b->n < 512 ? b->n : 512;
-    hipLaunchKernelGGL(w_env_step_list<128>, dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
-                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_ctl, b->d_ovf_total);
+    if (b->grasp) {
+      HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
+      /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier, whose
+         workgroup 0 also snapshots the routing hints for the next step */
+      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
+                         nullptr);
+      hipLaunchKernelGGL((w_env_step_list<128, KSL>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
+                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
+                         b->d_pred_ctl);
+    } else {
+      hipLaunchKernelGGL((w_env_step_list<128, KSL>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
+                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr);
+    }
   } else if (b->wave_nt == 128)
     hipLaunchKernelGGL((w_env_step<128, KSL>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
@@ -1944,6 +2061,14 @@ extern "C" int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* to
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(total, b->d_ovf_total, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts) {
+  if (!b || !counts) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(counts, b->d_ovf_total, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return UR3E_OK;
 }
 

@@ -158,6 +158,11 @@ struct KSX<MC, ME, NVC, TREE, true> {
   static constexpr int MAXEFC = ME;
   static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
   static constexpr bool BAIL = (MC < K_MAXCON) || (ME < K_MAXEFC);
+  /* constraint rows per lane of the register solver: row r lives on lane r % 64, slot r / 64 */
+  static constexpr int RPL = (ME + 63) / 64;
+  /* raw contacts one narrowphase chunk may stage (a chunk staging more has overflowed MAXCON) */
+  static constexpr int NPST = MC > W_NP_STAGE ? MC : W_NP_STAGE;
+  static_assert(RPL <= 2 && MC <= 64, "the register solver holds at most two rows per lane");
   /* ---- live for the whole env-step ---- */
   double qpos[K_NQ], qvel[K_NV], warm[K_NV], ctrl[K_NU];
   double xpos[K_NB][3];
@@ -200,8 +205,8 @@ struct KSX<MC, ME, NVC, TREE, true> {
         struct { /* KN, collision: clip polygons of one chunk of survivor lanes ([buf][vertex][coord]
                     [lane], conflict-free across lanes) and that chunk's staged raw contacts */
           double np_clip[2][8][3][W_NP_LANES];
-          double np_stage[7][W_NP_STAGE]; /* pos[3], n[3], dist */
-          int np_key[W_NP_STAGE];         /* survivor lane * 8 + contact index within the lane */
+          double np_stage[7][NPST]; /* pos[3], n[3], dist */
+          int np_key[NPST];         /* survivor lane * 8 + contact index within the lane */
           int np_nstage;
         };
       };
@@ -213,6 +218,9 @@ struct KSX<MC, ME, NVC, TREE, true> {
       int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
       double con_Hc[MC][9];
       double Hl[K_NV * (K_NV + 1) / 2];
+      /* ordered-sum slots of the register solver when rows span two lanes' slots (RPL 2); with
+         RPL 1 the three 64-double slots live in Hl (see R_SLOT) */
+      double rslot[RPL > 1 ? 3 * 64 * RPL : 1];
     };
   };
 };
@@ -240,6 +248,17 @@ typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
    so dof loops have constant trip counts and tree tests fold away */
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1> KSS_NV;
 static_assert(UR3E_MAIN_NV <= K_NV, "main.xml dofs exceed K_NV");
+/* grasp tier, between the compact and the full-capacity tier: the compact tier's code path (overlaid
+   LDS layout, register-resident solver with two rows per lane) sized for a firm grasp of the
+   box-surrogate pads, where main.xml reaches 12-20 contacts (C3 grasp and carry rows,
+   tools/contact_hist.py); its bails go on to the full-capacity tier */
+#ifndef W_GRASP_MAXCON
+#define W_GRASP_MAXCON 24
+#endif
+#ifndef W_GRASP_MAXEFC
+#define W_GRASP_MAXEFC 96
+#endif
+typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true> KSG_NV;
 #define NVOF(KS, m) ((KS::NV) ? (KS::NV) : (m)->nv)
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
@@ -692,6 +711,7 @@ struct KLdsClip {
     base[((buf * 8 + v) * 3 + c) * W_NP_LANES + ln] = x;
   }
 };
+template <int NST>
 struct KStageEmit {
   double* st;
   int* key;
@@ -699,10 +719,10 @@ struct KStageEmit {
   int ln;
   __device__ __forceinline__ void operator()(int k, const double pos[3], const double n[3], double dist) const {
     const int slot = atomicAdd(nst, 1);
-    if (slot < W_NP_STAGE) {
-      st[0 * W_NP_STAGE + slot] = pos[0]; st[1 * W_NP_STAGE + slot] = pos[1]; st[2 * W_NP_STAGE + slot] = pos[2];
-      st[3 * W_NP_STAGE + slot] = n[0]; st[4 * W_NP_STAGE + slot] = n[1]; st[5 * W_NP_STAGE + slot] = n[2];
-      st[6 * W_NP_STAGE + slot] = dist;
+    if (slot < NST) {
+      st[0 * NST + slot] = pos[0]; st[1 * NST + slot] = pos[1]; st[2 * NST + slot] = pos[2];
+      st[3 * NST + slot] = n[0]; st[4 * NST + slot] = n[1]; st[5 * NST + slot] = n[2];
+      st[6 * NST + slot] = dist;
       key[slot] = ln * 8 + k;
     }
   }
@@ -714,7 +734,7 @@ WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
   int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const KStageEmit emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
+  const KStageEmit<KS::NPST> emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
     return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2],
                          margin, emit);
@@ -774,7 +794,8 @@ WD void r_collision(KModel m, KS& s) {
     /* survivors in chunks of W_NP_LANES lanes: narrowphase with its clip polygons in LDS, raw
        contacts staged in LDS, then one lane per staged contact writes it at (prefix of its
        survivor lane) + (its index), the order of the pass below -- no private (scratch) arrays */
-    static_assert(KS::BAIL && KS::MAXCON <= W_NP_STAGE, "compact narrowphase stage must hold MAXCON");
+    constexpr int NST = KS::NPST;
+    static_assert(KS::BAIL && KS::MAXCON <= NST && NST <= 64, "compact narrowphase stage must hold MAXCON");
     if (lane == 0) s.np_nstage = 0;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
@@ -796,7 +817,7 @@ WD void r_collision(KModel m, KS& s) {
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       const int nall = s.np_nstage;
-      const int nst = nall < W_NP_STAGE ? nall : W_NP_STAGE;
+      const int nst = nall < NST ? nall : NST;
       const int key = lane < nst ? s.np_key[lane] : 0;
       const int src = key >> 3, kk = key & 7;
       const int offs = shfi(off, src), ps = shfi(p, src);
@@ -810,7 +831,7 @@ WD void r_collision(KModel m, KS& s) {
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       if (lane == 0) {
-        if (nall > W_NP_STAGE) s.ovf = 1; /* contacts were dropped from the stage: > MAXCON anyway */
+        if (nall > NST) s.ovf = 1; /* contacts were dropped from the stage: > MAXCON anyway */
         s.np_nstage = 0;
       }
       __builtin_amdgcn_wave_barrier();
@@ -938,7 +959,7 @@ template <int NT, class KS>
 WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
-  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64);
+  constexpr bool REG = (NT == 64 && KS::OVERLAY);
   if constexpr (REG) {
     r_mc_layout(m, pl, s);
     if (s.ovf) return;
@@ -1164,7 +1185,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int nb = m->nbody, nv = NVOF(KS, m);
   double (*cacc)[10] = s.u.body.b10;
   double (*cfrc)[6] = s.u.body.b6;
-  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64);
+  constexpr bool REG = (NT == 64 && KS::OVERLAY);
   if constexpr (REG) {
     r_cfrc(m, s); /* cacc came from r_vel_acc */
   } else {
@@ -1856,7 +1877,7 @@ template <int NT, class KS>
 WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
-  constexpr bool REG = (NT == 64 && KS::MAXEFC <= 64); /* compact tier: ur3e_wave_r.h */
+  constexpr bool REG = (NT == 64 && KS::OVERLAY); /* compact tier: ur3e_wave_r.h */
   static_assert(!KS::OVERLAY || REG, "the overlaid layout is only valid for the 64-lane register path");
   WT(23);
   if constexpr (REG) {

@@ -38,17 +38,39 @@ __device__ __forceinline__ double shf(double v, int src) {
 }
 __device__ __forceinline__ int shfi(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
 
-/* one constraint row per lane (lanes >= nefc: typ = -1, never contribute) */
+/* Constraint rows on the lanes: row r lives on lane r % 64 in slot r / 64 of the lane's RRow array
+   (KS::RPL slots: 1 for the compact tier, 2 for the grasp tier).  Lanes whose row is >= nefc have
+   typ = -1 and never contribute. */
 struct RRow {
-  int typ, jj, first; /* jj: row index inside its contact, first: lane of the contact's first row */
+  int typ, jj, first; /* jj: row index inside its contact, first: row index of the contact's first row */
   double D, R, aref, floss, mu, fr0, fr1;
   double jar, Jv, force, F; /* the Jacobian row stays in LDS (efc_J): 40 fewer live registers */
   int st, flag;
 };
 
+/* value of a per-row quantity at row `src` (any slot): a lane shuffle of the slot that holds it.
+   With one slot this is the plain shuffle (src 64, 65 wrap to lanes 0, 1 as before; never used). */
+template <int RPL>
+__device__ __forceinline__ double shfr(const double (&x)[RPL], int src) {
+  if constexpr (RPL == 1) {
+    return shf(x[0], src);
+  } else {
+    const double lo = shf(x[0], src & 63), hi = shf(x[1], src & 63);
+    return src < 64 ? lo : hi;
+  }
+}
+template <int RPL>
+__device__ __forceinline__ int shfri(const int (&x)[RPL], int src) {
+  if constexpr (RPL == 1) {
+    return shfi(x[0], src);
+  } else {
+    const int lo = shfi(x[0], src & 63), hi = shfi(x[1], src & 63);
+    return src < 64 ? lo : hi;
+  }
+}
+
 template <class KS>
-WD void r_load_rows(KModel m, const KS& s, RRow& w) {
-  const int r = w_lane();
+WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
   const int nefc = s.nefc;
   w.typ = -1; w.jj = 0; w.first = r;
   w.D = 0; w.R = 0; w.aref = 0; w.floss = 0; w.mu = 0; w.fr0 = 0; w.fr1 = 0;
@@ -71,83 +93,100 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w) {
 }
 
 /* mj_constraintUpdate per row (w_constraint_update) */
-WD void r_constraint_update(RRow& w) {
-  const double jar = w.jar, D = w.D, R = w.R;
-  /* contact cone: computed on every lane (uniform shuffles), used by contact lanes */
-  double jar1 = shf(jar, w_lane() + 1), jar2 = shf(jar, w_lane() + 2);
-  double mu = w.mu;
-  double U0 = jar * mu, U1 = jar1 * w.fr0, U2 = jar2 * w.fr1;
-  double N = U0;
-  double T2 = 0;
-  T2 += U1 * U1;
-  T2 += U2 * U2;
-  double T = sqrt(T2);
-  int z;
-  if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
-  else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
-  else z = 2;
-  double Dm = D / (mu * mu * (1 + mu * mu));
-  double NT_ = N - mu * T;
-  double Fm = 0.5 * Dm * NT_ * NT_;
-  double f0 = -Dm * NT_ * mu;
-  double f1 = Dm * NT_ * mu * U1 / T * w.fr0;
-  double f2 = Dm * NT_ * mu * U2 / T * w.fr1;
-  int zs = shfi(z, w.first);
-  double f1s = shf(f1, w.first), f2s = shf(f2, w.first);
-  const int t = w.typ;
-  if (t == CN_EQUALITY) {
-    w.force = -D * jar;
-    w.F = 0.5 * D * jar * jar; w.flag = 1;
-    w.st = ST_QUADRATIC;
-  } else if (t == CN_FRICTION_DOF) {
-    double fl = w.floss;
-    if (jar <= -R * fl) {
-      w.force = fl;
-      w.F = -0.5 * R * fl * fl - fl * jar;
-      w.st = ST_LINEARNEG;
-    } else if (jar >= R * fl) {
-      w.force = -fl;
-      w.F = -0.5 * R * fl * fl + fl * jar;
-      w.st = ST_LINEARPOS;
-    } else {
-      w.force = -D * jar;
-      w.F = 0.5 * D * jar * jar;
-      w.st = ST_QUADRATIC;
-    }
-    w.flag = 1;
-  } else if (t == CN_LIMIT_JOINT) {
-    if (jar >= 0) {
-      w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
-    } else {
+template <int RPL>
+WD void r_constraint_update(RRow (&W)[RPL]) {
+  const int lane = w_lane();
+  double jarv[RPL], f0v[RPL], f1v[RPL], f2v[RPL], Fmv[RPL];
+  int zv[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) jarv[h] = W[h].jar;
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    const RRow& w = W[h];
+    const int row = lane + 64 * h;
+    const double jar = w.jar, D = w.D;
+    /* contact cone: computed on every lane (uniform shuffles), used by contact lanes */
+    double jar1 = shfr(jarv, row + 1), jar2 = shfr(jarv, row + 2);
+    double mu = w.mu;
+    double U0 = jar * mu, U1 = jar1 * w.fr0, U2 = jar2 * w.fr1;
+    double N = U0;
+    double T2 = 0;
+    T2 += U1 * U1;
+    T2 += U2 * U2;
+    double T = sqrt(T2);
+    int z;
+    if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
+    else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
+    else z = 2;
+    double Dm = D / (mu * mu * (1 + mu * mu));
+    double NT_ = N - mu * T;
+    Fmv[h] = 0.5 * Dm * NT_ * NT_;
+    f0v[h] = -Dm * NT_ * mu;
+    f1v[h] = Dm * NT_ * mu * U1 / T * w.fr0;
+    f2v[h] = Dm * NT_ * mu * U2 / T * w.fr1;
+    zv[h] = z;
+  }
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    RRow& w = W[h];
+    const double jar = w.jar, D = w.D, R = w.R;
+    int zs = shfri(zv, w.first);
+    double f1s = shfr(f1v, w.first), f2s = shfr(f2v, w.first);
+    const int t = w.typ;
+    if (t == CN_EQUALITY) {
       w.force = -D * jar;
       w.F = 0.5 * D * jar * jar; w.flag = 1;
       w.st = ST_QUADRATIC;
-    }
-  } else if (t >= 0) {
-    if (zs == 0) {
-      w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
-    } else if (zs == 1) {
-      w.force = -D * jar;
-      w.F = 0.5 * D * jar * jar;
+    } else if (t == CN_FRICTION_DOF) {
+      double fl = w.floss;
+      if (jar <= -R * fl) {
+        w.force = fl;
+        w.F = -0.5 * R * fl * fl - fl * jar;
+        w.st = ST_LINEARNEG;
+      } else if (jar >= R * fl) {
+        w.force = -fl;
+        w.F = -0.5 * R * fl * fl + fl * jar;
+        w.st = ST_LINEARPOS;
+      } else {
+        w.force = -D * jar;
+        w.F = 0.5 * D * jar * jar;
+        w.st = ST_QUADRATIC;
+      }
       w.flag = 1;
-      w.st = ST_QUADRATIC;
+    } else if (t == CN_LIMIT_JOINT) {
+      if (jar >= 0) {
+        w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
+      } else {
+        w.force = -D * jar;
+        w.F = 0.5 * D * jar * jar; w.flag = 1;
+        w.st = ST_QUADRATIC;
+      }
+    } else if (t >= 0) {
+      if (zs == 0) {
+        w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
+      } else if (zs == 1) {
+        w.force = -D * jar;
+        w.F = 0.5 * D * jar * jar;
+        w.flag = 1;
+        w.st = ST_QUADRATIC;
+      } else {
+        w.st = ST_CONE;
+        if (w.jj == 0) { w.F = Fmv[h]; w.flag = 1; w.force = f0v[h]; }
+        else if (w.jj == 1) { w.flag = 0; w.force = f1s; }
+        else { w.flag = 0; w.force = f2s; }
+      }
     } else {
-      w.st = ST_CONE;
-      if (w.jj == 0) { w.F = Fm; w.flag = 1; w.force = f0; }
-      else if (w.jj == 1) { w.flag = 0; w.force = f1s; }
-      else { w.flag = 0; w.force = f2s; }
+      w.flag = 0; w.force = 0; w.st = ST_SATISFIED;
     }
-  } else {
-    w.flag = 0; w.force = 0; w.st = ST_SATISFIED;
   }
 }
 
-/* J[lane] . x in dof order, the row read from LDS (lanes >= nefc: a zero row, as the oracle's
+/* J[row] . x in dof order, the row read from LDS (rows >= nefc: a zero row, as the oracle's
    unused rows never enter a sum; +0 + 0*x stays +0) */
 template <class KS>
-WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV]) {
-  const bool act = w_lane() < nefc;
-  const int r = act ? w_lane() : 0;
+WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV], int row) {
+  const bool act = row < nefc;
+  const int r = act ? row : 0;
   double v = 0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++)
@@ -155,17 +194,31 @@ WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV]) {
   return v;
 }
 
-/* Ordered sums and vector broadcasts inside Newton go through a 64-double LDS slot per operand
-   (the packed-Hessian bytes, unused outside r_direction): each lane stores its value, then every
-   lane reads the slot in order with broadcast ds_reads, which issue back to back, instead of a
-   chain of v_readlane pairs.  Same operands, same order, so the sums are unchanged. */
-#define R_SLOT(s, k) ((s).Hl + 64 * (k))
+/* Ordered sums and vector broadcasts inside Newton go through a 64*RPL-double LDS slot per operand
+   (with one row slot per lane: the packed-Hessian bytes, unused outside r_direction): each lane
+   stores its value(s), then every lane reads the slot in order with broadcast ds_reads, which
+   issue back to back, instead of a chain of v_readlane pairs.  Same operands, same order, so the
+   sums are unchanged. */
+template <class KS>
+__device__ __forceinline__ double* r_slot_ptr(KS& s, int k) {
+  if constexpr (KS::RPL == 1) return s.Hl + 64 * k;
+  else return s.rslot + 64 * KS::RPL * k;
+}
+#define R_SLOT(s, k) r_slot_ptr(s, k)
 WD void r_stage(double* slot, double v) {
   slot[w_lane()] = v;
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
 WD void r_slot_done() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+/* every row slot of the lanes into `slot` (row r at slot[r]) */
+template <int RPL>
+WD void r_stage_rows(double* slot, const double (&v)[RPL]) {
+#pragma unroll
+  for (int h = 0; h < RPL; h++) slot[w_lane() + 64 * h] = v[h];
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
@@ -176,10 +229,11 @@ WD void r_bcast(double v, int nv, double out[K_NV]) {
   for (int k = 0; k < K_NV; k++) out[k] = k < nv ? rl(v, k) : 0.0;
 }
 
-/* w_eval_state: Ma (lane k), jar/force/cost terms (lane r), gauss and cost (uniform) */
+/* w_eval_state: Ma (lane k), jar/force/cost terms (per row), gauss and cost (uniform) */
 template <class KS>
-WD void r_eval_state(KModel m, KS& s, RRow& w, double qacc, double qs, double qas, double& Ma, double& gauss,
-                     double& cost) {
+WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs, double qas, double& Ma,
+                     double& gauss, double& cost) {
+  constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double qv[K_NV];
@@ -194,17 +248,20 @@ WD void r_eval_state(KModel m, KS& s, RRow& w, double qacc, double qs, double qa
       if (j < nv) v += qm_get(s, row, j) * qv[j];
     Ma = v;
   }
-  w.jar = r_row_dot(s, nv, nefc, qv) - w.aref;
-  r_constraint_update(w);
+#pragma unroll
+  for (int h = 0; h < RPL; h++) W[h].jar = r_row_dot(s, nv, nefc, qv, lane + 64 * h) - W[h].aref;
+  r_constraint_update(W);
   double term = (Ma - qs) * (qacc - qas);
   double a0 = 0, a1 = 0;
   /* skipped rows contribute -0.0: x + (-0.0) == x exactly for every x (incl. -0, inf, NaN), so
      the ordered sum needs neither a branch nor a select per row */
-  const double Fm0 = w.flag ? w.F : -0.0;
+  double Fm0[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) Fm0[h] = W[h].flag ? W[h].F : -0.0;
   double* st = R_SLOT(s, 1);
   double* sf = R_SLOT(s, 2);
   st[lane] = term;
-  r_stage(sf, Fm0);
+  r_stage_rows(sf, Fm0);
 #pragma unroll
   for (int i = 0; i < K_NV; i++)
     if (i < nv) a0 += st[i];
@@ -217,7 +274,9 @@ WD void r_eval_state(KModel m, KS& s, RRow& w, double qacc, double qs, double qa
 
 /* w_compute_grad: lane k: qfrc_constraint[k] = sum_i J[i][k] force[i] (row order), grad */
 template <class KS>
-WD void r_compute_grad(KModel m, KS& s, const RRow& w, double Ma, double qs, double& qfrc_c, double& grad) {
+WD void r_compute_grad(KModel m, KS& s, const RRow (&W)[KS::RPL], double Ma, double qs, double& qfrc_c,
+                       double& grad) {
+  constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nefc = s.nefc;
   const int col = lane < K_NV ? lane : 0;
@@ -225,7 +284,10 @@ WD void r_compute_grad(KModel m, KS& s, const RRow& w, double Ma, double qs, dou
   /* row forces broadcast from an LDS slot; partially unrolled: a fully unrolled MAXEFC-row loop
      hoists every J load at once */
   double* fs = R_SLOT(s, 0);
-  r_stage(fs, w.force);
+  double fv[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) fv[h] = W[h].force;
+  r_stage_rows(fs, fv);
 #pragma unroll 4
   for (int i = 0; i < nefc; i++) f = f + s.efc_J[i][col] * fs[i];
   r_slot_done();
@@ -236,37 +298,46 @@ WD void r_compute_grad(KModel m, KS& s, const RRow& w, double Ma, double qs, dou
 /* Newton direction: H = M + J'DJ + cone terms (lane k = row k), Cholesky in registers,
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
 template <class KS>
-WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
+WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
+  constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
-  /* cone Hessians (w_hessian_factor), on each contact's first-row lane */
+  /* cone Hessians (w_hessian_factor), on each contact's first row */
   {
-    double jar1 = shf(w.jar, lane + 1), jar2 = shf(w.jar, lane + 2);
-    if (w.typ >= 0 && w.typ != CN_EQUALITY && w.typ != CN_FRICTION_DOF && w.typ != CN_LIMIT_JOINT && w.jj == 0 &&
-        w.st == ST_CONE) {
-      int c = s.efc_id[lane];
-      double mu = w.mu;
-      double U[3], sc[3];
-      sc[0] = mu;
-      U[0] = w.jar * mu;
-      sc[1] = w.fr0; U[1] = jar1 * sc[1];
-      sc[2] = w.fr1; U[2] = jar2 * sc[2];
-      double T2 = 0;
-      for (int j = 1; j < 3; j++) T2 += U[j] * U[j];
-      double T = sqrt(T2);
-      double N = U[0];
-      double Dm = w.D / (mu * mu * (1 + mu * mu));
-      double Hc[3][3];
-      Hc[0][0] = 1;
-      for (int j = 1; j < 3; j++) {
-        Hc[0][j] = -mu * U[j] / T;
-        Hc[j][0] = Hc[0][j];
+    double jarv[RPL];
+#pragma unroll
+    for (int h = 0; h < RPL; h++) jarv[h] = W[h].jar;
+#pragma unroll
+    for (int h = 0; h < RPL; h++) {
+      const RRow& w = W[h];
+      const int rowi = lane + 64 * h;
+      double jar1 = shfr(jarv, rowi + 1), jar2 = shfr(jarv, rowi + 2);
+      if (w.typ >= 0 && w.typ != CN_EQUALITY && w.typ != CN_FRICTION_DOF && w.typ != CN_LIMIT_JOINT &&
+          w.jj == 0 && w.st == ST_CONE) {
+        int c = s.efc_id[rowi];
+        double mu = w.mu;
+        double U[3], sc[3];
+        sc[0] = mu;
+        U[0] = w.jar * mu;
+        sc[1] = w.fr0; U[1] = jar1 * sc[1];
+        sc[2] = w.fr1; U[2] = jar2 * sc[2];
+        double T2 = 0;
+        for (int j = 1; j < 3; j++) T2 += U[j] * U[j];
+        double T = sqrt(T2);
+        double N = U[0];
+        double Dm = w.D / (mu * mu * (1 + mu * mu));
+        double Hc[3][3];
+        Hc[0][0] = 1;
+        for (int j = 1; j < 3; j++) {
+          Hc[0][j] = -mu * U[j] / T;
+          Hc[j][0] = Hc[0][j];
+        }
+        double muNT = mu * N / T;
+        for (int j = 1; j < 3; j++)
+          for (int k = 1; k < 3; k++) Hc[j][k] = (j == k ? mu * mu - muNT : 0.0) + muNT * U[j] * U[k] / T2;
+        for (int j = 0; j < 3; j++)
+          for (int k = 0; k < 3; k++) s.con_Hc[c][3 * j + k] = Hc[j][k] * Dm * sc[j] * sc[k];
       }
-      double muNT = mu * N / T;
-      for (int j = 1; j < 3; j++)
-        for (int k = 1; k < 3; k++) Hc[j][k] = (j == k ? mu * mu - muNT : 0.0) + muNT * U[j] * U[k] / T2;
-      for (int j = 0; j < 3; j++)
-        for (int k = 0; k < 3; k++) s.con_Hc[c][3 * j + k] = Hc[j][k] * Dm * sc[j] * sc[k];
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -292,53 +363,59 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
     ec[q] = ev[q] ? e - k * (k + 1) / 2 : 0;
     hv[q] = s.qMp[ev[q] ? e : 0]; /* element e of the packed lower triangle is (ek, ec) */
   }
-  /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
-     compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
-     trips per element) */
   /* only rows that add to H are visited, in row order (the others add nothing in the oracle):
-     quadratic rows and the first row of each cone-state contact */
-  const bool adds = lane < nefc && (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC &&
-                                                               w.jj == 0));
-  unsigned long long act = __ballot(adds);
-  const int ifirst = act ? (int)__builtin_ctzll(act) : 0;
-  double njk[NQ], njc[NQ];
+     quadratic rows and the first row of each cone-state contact; slot h covers rows 64h.. */
 #pragma unroll
-  for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[ifirst][ek[q]]; njc[q] = s.efc_J[ifirst][ec[q]]; }
-  while (act) {
-    const int i = (int)__builtin_ctzll(act);
-    act &= act - 1;
-    double jk[NQ], jc[NQ];
+  for (int h = 0; h < RPL; h++) {
+    const RRow& w = W[h];
+    const int rb = 64 * h;
+    const bool adds = lane + rb < nefc &&
+                      (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC && w.jj == 0));
+    unsigned long long act = __ballot(adds);
+    /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
+       compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
+       trips per element) */
+    const int ifirst = act ? (int)__builtin_ctzll(act) : 0;
+    double njk[NQ], njc[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      jk[q] = njk[q]; jc[q] = njc[q];
-      asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
-    }
-    const int inext = act ? (int)__builtin_ctzll(act) : i;
-#pragma unroll
-    for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[inext][ek[q]]; njc[q] = s.efc_J[inext][ec[q]]; }
-    const int st = rli(w.st, i);
-    if (st == ST_QUADRATIC) {
-      const double D = rl(w.D, i);
+    for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[rb + ifirst][ek[q]]; njc[q] = s.efc_J[rb + ifirst][ec[q]]; }
+    while (act) {
+      const int i = (int)__builtin_ctzll(act);
+      act &= act - 1;
+      double jk[NQ], jc[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; q++) {
-        const double djr = D * jk[q];
-        double n = hv[q] + djr * jc[q];
-        asm volatile("" : "+v"(n));
-        hv[q] = jk[q] != 0 ? n : hv[q];
+        jk[q] = njk[q]; jc[q] = njc[q];
+        asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
       }
-    } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
-      const double* Hc = s.con_Hc[s.efc_id[i]];
+      const int inext = act ? (int)__builtin_ctzll(act) : i;
 #pragma unroll
-      for (int q = 0; q < NQ; q++) {
-        double t[3];
-        for (int j = 0; j < 3; j++) {
-          double acc = 0;
-          for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[i + k][ek[q]];
-          t[j] = acc;
+      for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[rb + inext][ek[q]]; njc[q] = s.efc_J[rb + inext][ec[q]]; }
+      const int st = rli(w.st, i);
+      if (st == ST_QUADRATIC) {
+        const double D = rl(w.D, i);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          const double djr = D * jk[q];
+          double n = hv[q] + djr * jc[q];
+          asm volatile("" : "+v"(n));
+          hv[q] = jk[q] != 0 ? n : hv[q];
         }
-        double acc = 0;
-        for (int j = 0; j < 3; j++) acc += s.efc_J[i + j][ec[q]] * t[j];
-        hv[q] += acc;
+      } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
+        const int ri = rb + i;
+        const double* Hc = s.con_Hc[s.efc_id[ri]];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          double t[3];
+          for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[ri + k][ek[q]];
+            t[j] = acc;
+          }
+          double acc = 0;
+          for (int j = 0; j < 3; j++) acc += s.efc_J[ri + j][ec[q]] * t[j];
+          hv[q] += acc;
+        }
       }
     }
   }
@@ -421,83 +498,108 @@ WD double r_direction(KModel m, KS& s, const RRow& w, double grad) {
 struct RLs {
   double jar1, jar2, Jv1, Jv2, V0, V1, V2, VV, Dm;
 };
-WD RLs r_ls_setup(const RRow& w) {
+template <int RPL>
+WD void r_ls_setup(const RRow (&W)[RPL], RLs (&C)[RPL]) {
   const int lane = w_lane();
-  RLs c;
-  c.jar1 = shf(w.jar, lane + 1); c.jar2 = shf(w.jar, lane + 2);
-  c.Jv1 = shf(w.Jv, lane + 1); c.Jv2 = shf(w.Jv, lane + 2);
-  const double mu = w.mu;
-  c.V0 = w.Jv * mu;
-  c.V1 = c.Jv1 * w.fr0;
-  c.V2 = c.Jv2 * w.fr1;
-  c.VV = 0;
-  c.VV += c.V1 * c.V1;
-  c.VV += c.V2 * c.V2;
-  c.Dm = w.D / (mu * mu * (1 + mu * mu));
-  return c;
+  double jarv[RPL], jvv[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) { jarv[h] = W[h].jar; jvv[h] = W[h].Jv; }
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    const RRow& w = W[h];
+    RLs& c = C[h];
+    const int row = lane + 64 * h;
+    c.jar1 = shfr(jarv, row + 1); c.jar2 = shfr(jarv, row + 2);
+    c.Jv1 = shfr(jvv, row + 1); c.Jv2 = shfr(jvv, row + 2);
+    const double mu = w.mu;
+    c.V0 = w.Jv * mu;
+    c.V1 = c.Jv1 * w.fr0;
+    c.V2 = c.Jv2 * w.fr1;
+    c.VV = 0;
+    c.VV += c.V1 * c.V1;
+    c.VV += c.V2 * c.V2;
+    c.Dm = w.D / (mu * mu * (1 + mu * mu));
+  }
 }
 
 template <class KS>
-WD void r_ls_eval(KS& s, const RRow& w, const RLs& c, int nefc, double a, double gauss, double g1, double g2,
-                  double& lsF, double& lsdF, double& lsd2F) {
-  const int lane = w_lane();
-  const double D = w.D, R = w.R;
-  double x = w.jar + a * w.Jv;
-  double v = w.Jv;
-  /* cone terms from the contact's first row (computed everywhere, used by contact lanes) */
-  const double jar1 = c.jar1, jar2 = c.jar2, Jv1 = c.Jv1, Jv2 = c.Jv2;
-  double mu = w.mu;
-  double U0 = (w.jar + a * w.Jv) * mu, V0 = c.V0;
-  double U1 = (jar1 + a * Jv1) * w.fr0, V1 = c.V1;
-  double U2 = (jar2 + a * Jv2) * w.fr1, V2 = c.V2;
-  double N = U0;
-  double T2 = 0;
-  T2 += U1 * U1;
-  T2 += U2 * U2;
-  double T = sqrt(T2);
-  int z;
-  if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
-  else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
-  else z = 2;
-  const double Dm = c.Dm, VV = c.VV;
-  double UV = 0;
-  UV += U1 * V1;
-  UV += U2 * V2;
-  double NT_ = N - mu * T;
-  double dNT = V0 - mu * UV / T;
-  double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
-  double cF = 0.5 * Dm * NT_ * NT_;
-  double cdF = Dm * NT_ * dNT;
-  double cd2F = Dm * (dNT * dNT + NT_ * d2NT);
-  int zs = shfi(z, w.first);
-  double F = 0, dF = 0, d2F = 0;
-  int flag = 0;
-  const int t = w.typ;
-  if (t == CN_EQUALITY) {
-    F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
-  } else if (t == CN_FRICTION_DOF) {
-    double fl = w.floss;
-    if (x <= -R * fl) { F = -0.5 * R * fl * fl - fl * x; dF = -fl * v; flag = 2; }
-    else if (x >= R * fl) { F = -0.5 * R * fl * fl + fl * x; dF = fl * v; flag = 2; }
-    else { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
-  } else if (t == CN_LIMIT_JOINT) {
-    if (x < 0) { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
-  } else if (t >= 0) {
-    if (zs == 1) {
+WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int nefc, double a, double gauss,
+                  double g1, double g2, double& lsF, double& lsdF, double& lsd2F) {
+  constexpr int RPL = KS::RPL;
+  int zv[RPL];
+  double cFv[RPL], cdFv[RPL], cd2Fv[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    const RRow& w = W[h];
+    const RLs& c = C[h];
+    /* cone terms from the contact's first row (computed everywhere, used by contact lanes) */
+    const double jar1 = c.jar1, jar2 = c.jar2, Jv1 = c.Jv1, Jv2 = c.Jv2;
+    double mu = w.mu;
+    double U0 = (w.jar + a * w.Jv) * mu, V0 = c.V0;
+    double U1 = (jar1 + a * Jv1) * w.fr0, V1 = c.V1;
+    double U2 = (jar2 + a * Jv2) * w.fr1, V2 = c.V2;
+    double N = U0;
+    double T2 = 0;
+    T2 += U1 * U1;
+    T2 += U2 * U2;
+    double T = sqrt(T2);
+    int z;
+    if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
+    else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
+    else z = 2;
+    const double Dm = c.Dm, VV = c.VV;
+    double UV = 0;
+    UV += U1 * V1;
+    UV += U2 * V2;
+    double NT_ = N - mu * T;
+    double dNT = V0 - mu * UV / T;
+    double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
+    cFv[h] = 0.5 * Dm * NT_ * NT_;
+    cdFv[h] = Dm * NT_ * dNT;
+    cd2Fv[h] = Dm * (dNT * dNT + NT_ * d2NT);
+    zv[h] = z;
+  }
+  double Fm[RPL], dFm[RPL], d2Fm[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    const RRow& w = W[h];
+    const double D = w.D, R = w.R;
+    double x = w.jar + a * w.Jv;
+    double v = w.Jv;
+    int zs = shfri(zv, w.first);
+    double F = 0, dF = 0, d2F = 0;
+    int flag = 0;
+    const int t = w.typ;
+    if (t == CN_EQUALITY) {
       F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
-    } else if (zs == 2 && w.jj == 0) {
-      F = cF; dF = cdF; d2F = cd2F; flag = 1;
+    } else if (t == CN_FRICTION_DOF) {
+      double fl = w.floss;
+      if (x <= -R * fl) { F = -0.5 * R * fl * fl - fl * x; dF = -fl * v; flag = 2; }
+      else if (x >= R * fl) { F = -0.5 * R * fl * fl + fl * x; dF = fl * v; flag = 2; }
+      else { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+    } else if (t == CN_LIMIT_JOINT) {
+      if (x < 0) { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
+    } else if (t >= 0) {
+      if (zs == 1) {
+        F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
+      } else if (zs == 2 && w.jj == 0) {
+        F = cFv[h]; dF = cdFv[h]; d2F = cd2Fv[h]; flag = 1;
+      }
     }
+    /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
+    Fm[h] = flag ? F : -0.0; dFm[h] = flag ? dF : -0.0; d2Fm[h] = flag == 1 ? d2F : -0.0;
   }
   double aF = gauss + a * g1 + 0.5 * a * a * g2;
   double adF = g1 + a * g2;
   double ad2F = g2;
-  /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
-  const double Fm = flag ? F : -0.0, dFm = flag ? dF : -0.0, d2Fm = flag == 1 ? d2F : -0.0;
   double *b0 = R_SLOT(s, 0), *b1 = R_SLOT(s, 1), *b2 = R_SLOT(s, 2);
-  b0[lane] = Fm;
-  b1[lane] = dFm;
-  r_stage(b2, d2Fm);
+  const int lane = w_lane();
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    b0[lane + 64 * h] = Fm[h];
+    b1[lane + 64 * h] = dFm[h];
+  }
+  r_stage_rows(b2, d2Fm);
 #pragma unroll 4
   for (int i = 0; i < nefc; i++) {
     aF += b0[i];
@@ -510,8 +612,9 @@ WD void r_ls_eval(KS& s, const RRow& w, const RLs& c, int nefc, double a, double
 
 /* w_line_search: returns alpha (uniform); Jv on the row lanes */
 template <class KS>
-WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, double qs, double gauss,
+WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, double Ma, double qs, double gauss,
                         double scale) {
+  constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
   double sv[K_NV];
@@ -533,7 +636,8 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
       if (j < nv) v += qm_get(s, row, j) * sv[j];
     Mv = v;
   }
-  w.Jv = r_row_dot(s, nv, nefc, sv);
+#pragma unroll
+  for (int h = 0; h < RPL; h++) W[h].Jv = r_row_dot(s, nv, nefc, sv, lane + 64 * h);
   if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
   double g1 = 0, g2 = 0;
@@ -549,8 +653,9 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   r_slot_done();
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
-  const RLs lc = r_ls_setup(w);
-  r_ls_eval(s, w, lc, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
+  RLs lc[RPL];
+  r_ls_setup(W, lc);
+  r_ls_eval(s, W, lc, nefc, 0.0, gauss, g1, g2, f0, d0, h0);
   if (d0 >= 0) return 0;
   double lo = 0.0, dlo = d0, hlo = h0;
   double hi = -1.0, dhi = 0, hhi = 0;
@@ -559,7 +664,7 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
   WT(19);
   for (int it = 0; it < m->ls_iterations; it++) {
     double f, df, d2f;
-    r_ls_eval(s, w, lc, nefc, a, gauss, g1, g2, f, df, d2f);
+    r_ls_eval(s, W, lc, nefc, a, gauss, g1, g2, f, df, d2f);
     WT(20);
     if (f < bestF) { bestF = f; bestA = a; }
     if (fabs(df) < gtol) return (f <= bestF) ? a : bestA;
@@ -584,6 +689,7 @@ WD double r_line_search(KModel m, KS& s, RRow& w, double search, double Ma, doub
 /* w_solve_newton for the compact tier; leaves s.qacc and s.qfrc_constraint */
 template <class KS>
 WD void r_solve_newton(KModel m, KS& s) {
+  constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m);
   if (s.nefc == 0) {
@@ -596,31 +702,32 @@ WD void r_solve_newton(KModel m, KS& s) {
   const int k = lane < nv ? lane : 0;
   const double qs = s.qfrc_smooth[k], qas = s.qacc_smooth[k];
   double qacc = lane < nv ? s.warm[k] : 0.0;
-  RRow w;
-  r_load_rows(m, s, w);
+  RRow W[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) r_load_rows(m, s, W[h], lane + 64 * h);
   double Ma, gauss, cost;
-  r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
+  r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
   const double cost_ws = cost;
-  r_eval_state(m, s, w, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost);
+  r_eval_state(m, s, W, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost);
   const double cost_sm = cost;
   if (cost_ws > cost_sm) {
     qacc = lane < nv ? qas : 0.0;
   } else {
-    r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
+    r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
   }
   double qfrc_c, grad;
-  r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
+  r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad);
   WT(9);
-  double search = r_direction(m, s, w, grad);
+  double search = r_direction(m, s, W, grad);
   WT(11);
   for (int iter = 0; iter < m->iterations; iter++) {
-    double alpha = r_line_search(m, s, w, search, Ma, qs, gauss, scale);
+    double alpha = r_line_search(m, s, W, search, Ma, qs, gauss, scale);
     WT(13);
     if (alpha == 0) break;
     qacc += alpha * search;
     double oldcost = cost;
-    r_eval_state(m, s, w, qacc, qs, qas, Ma, gauss, cost);
-    r_compute_grad(m, s, w, Ma, qs, qfrc_c, grad);
+    r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
+    r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad);
     WT(14);
     double gn = 0;
     r_stage(R_SLOT(s, 0), grad);
@@ -634,11 +741,14 @@ WD void r_solve_newton(KModel m, KS& s) {
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
-    search = r_direction(m, s, w, grad);
+    search = r_direction(m, s, W, grad);
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
-  if (lane < s.nefc) s.efc_force[lane] = w.force; /* touch sensors read the contact normal forces */
+  /* touch sensors read the contact normal forces */
+#pragma unroll
+  for (int h = 0; h < RPL; h++)
+    if (lane + 64 * h < s.nefc) s.efc_force[lane + 64 * h] = W[h].force;
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
@@ -1013,7 +1123,8 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int ncg = __popcll(mc);
   const int nrow = nfixrow + nlim + 3 * ncg;
   const int ngrp = nfix + nlim + ncg;
-  if (nrow > KS::MAXEFC) {
+  /* rows beyond the tier's capacity, or more groups than lanes (lane = group below), bail */
+  if (nrow > KS::MAXEFC || ngrp > 64) {
     if (lane == 0) s.ovf = 1;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
@@ -1195,11 +1306,12 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
-  /* ---- 3. impedance, lane = row (w_row_impedance) ---- */
-  {
-    const int r = lane;
-    const int g = lane < nefc ? s.efc_grp[r] : 0;
-    const int k = lane < nefc ? r - s.grp_row[g] : 0;
+  /* ---- 3. impedance, lane = row (w_row_impedance); row lane + 64 h for each row slot ---- */
+#pragma unroll
+  for (int h = 0; h < KS::RPL; h++) {
+    const int r = lane + 64 * h;
+    const int g = r < nefc ? s.efc_grp[r] : 0;
+    const int k = r < nefc ? r - s.grp_row[g] : 0;
     const double p0 = shf(gpos[0], g), p1 = shf(gpos[1], g), p2 = shf(gpos[2], g);
     const double pos = k == 0 ? p0 : (k == 1 ? p1 : p2);
     const double margin = shf(gmargin, g), diag = shf(gdiag, g);
@@ -1208,7 +1320,7 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
     double sr[2], si[5];
     for (int q = 0; q < 2; q++) sr[q] = shf(sref[q], g);
     for (int q = 0; q < 5; q++) si[q] = shf(simp[q], g);
-    if (lane < nefc) {
+    if (r < nefc) {
       double jr[K_NV], qv[K_NV];
 #pragma unroll
       for (int q = 0; q < K_NV; q++) { jr[q] = s.efc_J[r][q]; qv[q] = s.qvel[q]; }

@@ -72,6 +72,7 @@ def load_library():
     L.ur3e_batch_last_step_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.ur3e_batch_set_timing.argtypes = [vp, ip]
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ur3e_batch_tier_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
@@ -257,6 +258,13 @@ class Batch:
         out = self.torch.zeros((self.n, nt), dtype=self.torch.float64, device=self.device)
         _check(self.L.ur3e_batch_get_touch(self.h, _ptr(out), self._stream()))
         return out[:, :self.model_c.ntouch]
+
+    def tier_counts(self) -> tuple:
+        """Since create: (env-steps the compact tier handed to the grasp tier, env-steps the grasp tier
+        handed to the full-capacity tier, env-steps routed straight to the grasp tier)."""
+        v = (ctypes.c_ulonglong * 3)()
+        _check(self.L.ur3e_batch_tier_counts(self.h, v))
+        return int(v[0]), int(v[1]), int(v[2])
 
     def overflow_count(self) -> int:
         """Env-steps the compact tier handed to the full-capacity tier since create."""
