@@ -168,7 +168,8 @@ int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 
 /* since create (synchronises): counts[0] env-steps the compact tier handed on to the grasp tier,
    counts[1] env-steps the grasp tier handed on to the full-capacity tier, counts[2] env-steps routed
-   straight to the grasp tier (the env's previous forward had more than 8 contacts; it runs on an
+   straight to the grasp tier (the env's previous forward had more than 8 contacts or 36 constraint
+   rows; it runs on an
    internal stream concurrently with the compact tier) */
 int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
 

@@ -1,5 +1,10 @@
-"""Diagnostic: per-stage cycle breakdown of the v2 step kernel (separate -DUR3E_STAGE_TIMING build).
-Never quote this build's run time (its atomics serialise lane 0); read the SHARES."""
+"""Diagnostic: per-stage cycle breakdown of the v2 step kernels (separate -DUR3E_STAGE_TIMING build).
+Never quote this build's run time (its atomics serialise lane 0); read the SHARES.
+
+usage: stage_timing.py [n_envs] [envs_per_block] [workload: gym | c3] [tier: 0 compact | 1 grasp | 2 full]
+  gym: gym ur3e-v2 random actions (2 substeps, per-env-step launch so the stage marks run);
+  c3:  the scripted move_l_mug pick (1 substep per row) timed over its grasp rows 1850..2100, where
+       routed envs run in the grasp tier."""
 import ctypes, os, subprocess, sys
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, REPO)
@@ -19,25 +24,42 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
          15: "newton tail", 21: "touch sensors", 22: "badacc check", 16: "euler factor+solve", 17: "integrate", 25: "make_carry", 26: "obs+reward+termination", 27: "commit"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-md, mc = rt.load_model("main")
-b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1, envs_per_block=epb, schedule=1), n)  # schedule 1: per-env-step kernel (the one with stage marks)
+work = sys.argv[3] if len(sys.argv) > 3 else "gym"
+tier = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 L = rt.load_library()
+L.ur3e_debug_stage_cycles_tier.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 cyc = (ctypes.c_ulonglong * 32)(); calls = (ctypes.c_ulonglong * 32)()
-lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")
-hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device="cuda")
-for i in range(3):
-    b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
+if work == "gym":
+    md, mc = rt.load_model("main")
+    # schedule 1: the per-env-step kernel (the one with stage marks)
+    b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1, envs_per_block=epb,
+                                    schedule=1), n)
+    lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")
+    hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device="cuda")
+    for i in range(3):
+        b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
+    K, subs = 5, 2
+    steps = [lambda: b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))] * K
+else:
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    drv = MoveLMug(n, reset_mode="low", seed=0)
+    b = drv.batch
+    r0, K, subs = 1850, 250, 1
+    for t in range(r0):
+        b.step(drv.traj.row(t))
+    steps = [(lambda t=t: b.step(drv.traj.row(t))) for t in range(r0, r0 + K)]
 torch.cuda.synchronize()
-L.ur3e_debug_stage_cycles(cyc, calls, 1)
-K = 5
-for i in range(K):
-    b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
+L.ur3e_debug_stage_cycles_tier(tier, cyc, calls, 1)
+for f in steps:
+    f()
 torch.cuda.synchronize()
-L.ur3e_debug_stage_cycles(cyc, calls, 1)
+L.ur3e_debug_stage_cycles_tier(tier, cyc, calls, 1)
 tot = sum(cyc[k] for k in names)
-print(f"per env-substep cycles (lane 0 view), {n} envs, {K} steps")
+units = calls[23] if calls[23] else 1  # forward passes run (substeps + retries + resets)
+print(f"tier {tier}, workload {work}: per-forward cycles (lane 0 view), {n} envs, {K} steps, "
+      f"{calls[23]} forward passes in this tier")
 for k, nm in names.items():
     if calls[k]:
-        per = cyc[k] / (n * K * 2)
-        print(f"{k:2d} {nm:32s} {per:12.0f} cyc/env-substep  {100.0 * cyc[k] / tot:5.1f}%  calls/env-substep {calls[k] / (n * K * 2):.2f}")
-print("total", tot / (n * K * 2))
+        per = cyc[k] / units
+        print(f"{k:2d} {nm:32s} {per:12.0f} cyc/forward  {100.0 * cyc[k] / tot:5.1f}%  calls/forward {calls[k] / units:.2f}")
+print("total per forward", tot / units)

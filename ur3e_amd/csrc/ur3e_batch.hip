@@ -392,8 +392,11 @@ struct KState {
   unsigned char* hint;
   unsigned char* route;
 };
-/* an env whose last forward had more contacts than this runs its next step in the grasp tier */
+/* an env whose last forward had more contacts or constraint rows than these runs its next step in
+   the grasp tier (the compact tier holds 10 contacts / 44 rows; the margin covers the contacts and
+   joint-limit rows one step can add) */
 #define W_ROUTE_NCON 8
+#define W_ROUTE_NEFC 36
 
 struct KConfig {
   int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
@@ -870,7 +873,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   const int od = k_obs_dim(c.task);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
-    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > W_ROUTE_NCON);
+    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > W_ROUTE_NCON || s.nefc > W_ROUTE_NEFC);
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
     if (stepped && k_is_gym(c.task)) {
       if (rew_out) rew_out[e] = o.r;
@@ -1401,7 +1404,10 @@ __global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __r
   const int cnt = s_cnt;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int e = ovf_list[i];
-    if (w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
+    WT_INIT();
+    const int r = w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
+    WT_FLUSH();
+    if (r == W_BAIL) {
       if constexpr (KS::BAIL) {
         if (threadIdx.x == 0) {
           const int slot = atomicAdd(next_ctl, 1);
@@ -1732,7 +1738,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMemset(s.hint, 0, nd));
     HIPCHK(hipMalloc(&s.route, nd));
     HIPCHK(hipMemset(s.route, 0, nd));
-    HIPCHK(hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking));
+    /* high priority: the routed envs are the long ones, so their workgroups should be dispatched
+       before the compact tier's fill the CUs */
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
   }
@@ -2026,21 +2036,30 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
 }
 
 /* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */
-extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {
+extern "C" int ur3e_debug_stage_cycles_tier(int tier, unsigned long long* cycles, unsigned long long* calls,
+                                            int reset) {
 #ifdef UR3E_STAGE_TIMING
+  if (tier < 0 || tier > 2) return fail(UR3E_EINVAL, "tier must be 0 (compact), 1 (grasp) or 2 (full)");
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(cycles, HIP_SYMBOL(ur3e_stage_cycles), sizeof(unsigned long long) * 32));
-  HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(ur3e_stage_calls), sizeof(unsigned long long) * 32));
+  unsigned long long c[3][32], k[3][32];
+  HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(ur3e_stage_cycles), sizeof(c)));
+  HIPCHK(hipMemcpyFromSymbol(k, HIP_SYMBOL(ur3e_stage_calls), sizeof(k)));
+  for (int i = 0; i < 32; i++) { cycles[i] = c[tier][i]; calls[i] = k[tier][i]; }
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[3][32] = {{0}};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_cycles), z, sizeof(z)));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_calls), z, sizeof(z)));
   }
   return UR3E_OK;
 #else
-  (void)cycles; (void)calls; (void)reset;
+  (void)tier; (void)cycles; (void)calls; (void)reset;
   return fail(UR3E_EINVAL, "library built without -DUR3E_STAGE_TIMING");
 #endif
+}
+
+/* diagnostics: per-stage cycle totals of the compact tier (-DUR3E_STAGE_TIMING build) */
+extern "C" int ur3e_debug_stage_cycles(unsigned long long* cycles, unsigned long long* calls, int reset) {
+  return ur3e_debug_stage_cycles_tier(0, cycles, calls, reset);
 }
 
 /* diagnostic: copy the wave trace of the last step launch (UR3E_WAVE_TRACE builds only) */

@@ -290,8 +290,14 @@ __device__ __forceinline__ int w_any(int pred) {
 
 /* diagnostic build only (-DUR3E_STAGE_TIMING): per-stage shader-clock cycles, lane 0 of every env */
 #ifdef UR3E_STAGE_TIMING
-__device__ unsigned long long ur3e_stage_cycles[32];
-__device__ unsigned long long ur3e_stage_calls[32];
+/* [tier][stage]: tier 0 compact (KS::MAXCON <= W_SMALL_MAXCON), 1 grasp (other overlaid layouts),
+   2 full capacity */
+__device__ unsigned long long ur3e_stage_cycles[3][32];
+__device__ unsigned long long ur3e_stage_calls[3][32];
+#define W_TIER_OF(s)                                                                          \
+  (std::remove_reference_t<decltype(s)>::MAXCON <= W_SMALL_MAXCON                           \
+       ? 0                                                                                   \
+       : (std::remove_reference_t<decltype(s)>::OVERLAY ? 1 : 2))
 /* accumulated per wave in LDS and flushed once at kernel end: a global atomic per mark would sit in
    the wave's vmcnt queue and bill its (contended) latency to the next stage that loads from memory */
 #define WT(k)                                                           \
@@ -315,8 +321,8 @@ __device__ unsigned long long ur3e_stage_calls[32];
   do {                                                                  \
     __builtin_amdgcn_wave_barrier();                                    \
     if (w_lane() < 32 && s.tcnt[w_lane()]) {                      \
-      atomicAdd(&ur3e_stage_cycles[w_lane()], (unsigned long long)s.tacc[w_lane()]);  \
-      atomicAdd(&ur3e_stage_calls[w_lane()], (unsigned long long)s.tcnt[w_lane()]); \
+      atomicAdd(&ur3e_stage_cycles[W_TIER_OF(s)][w_lane()], (unsigned long long)s.tacc[w_lane()]);  \
+      atomicAdd(&ur3e_stage_calls[W_TIER_OF(s)][w_lane()], (unsigned long long)s.tcnt[w_lane()]); \
     }                                                                   \
   } while (0)
 #else
