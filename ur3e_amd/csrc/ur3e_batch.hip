@@ -856,9 +856,10 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
 }
 
 /* the single write-back point of every v2 kernel */
-template <int NT, class KS>
+template <int NT, int TK = -1, class KS>
 WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& s, const WOut& o, double* obs_out,
                  double* rew_out, unsigned char* term_out, unsigned char* trunc_out, double* tobs_out, int stepped) {
+  const int TASK = TK >= 0 ? TK : c.task; /* TK >= 0: kernel specialised for one task at compile time */
   const int tid = w_lane();
   for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
@@ -870,22 +871,22 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
       for (int k = tid; k < m->nsensordata; k += NT)
         st.sensordata[(size_t)e * UR3E_MAXSENSORDATA + k] = s.sensordata[k];
   }
-  const int od = k_obs_dim(c.task);
+  const int od = k_obs_dim(TASK);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
     if (st.hint) st.hint[e] = (unsigned char)(s.ncon > W_ROUTE_NCON || s.nefc > W_ROUTE_NEFC);
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
-    if (stepped && k_is_gym(c.task)) {
+    if (stepped && k_is_gym(TASK)) {
       if (rew_out) rew_out[e] = o.r;
       if (term_out) term_out[e] = (unsigned char)o.term;
       if (trunc_out) trunc_out[e] = (unsigned char)o.trunc;
     }
   }
-  if (k_is_gym(c.task)) {
+  if (k_is_gym(TASK)) {
     if (stepped && o.did_reset && tobs_out)
       for (int k = tid; k < od; k += NT) tobs_out[(size_t)e * od + k] = o.tobs[k];
   }
-  if (obs_out && (k_is_gym(c.task) || c.obs_sites))
+  if (obs_out && (k_is_gym(TASK) || c.obs_sites))
     for (int k = tid; k < od; k += NT) obs_out[(size_t)e * od + k] = o.obs[k];
 }
 
@@ -917,20 +918,21 @@ WD void w_reset_prep(KModel m, const KConfig& c, int e, KS& s, WOut& o) {
   SYNC();
 }
 
-template <int NT, class KS>
+template <int NT, int TK = -1, class KS>
 WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c, KS& s, WOut& o) {
+  const int TASK = TK >= 0 ? TK : c.task; /* TK >= 0: kernel specialised for one task at compile time */
   const int tid = w_lane();
-  if (tid == 0 && (k_is_gym(c.task) || c.obs_sites)) w_task_obs(m, s, c.task, o.obs);
+  if (tid == 0 && (k_is_gym(TASK) || c.obs_sites)) w_task_obs(m, s, TASK, o.obs);
   w_make_carry<NT>(m, pl, s, o.carry);
   SYNC();
 }
 
-template <int NT, class KS>
+template <int NT, int TK = -1, class KS>
 WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, int e, KS& s, WOut& o) {
   w_reset_prep<NT>(m, c, e, s, o);
   w_forward<NT>(m, pl, s);
   if (KS::BAIL && s.ovf) return;
-  w_reset_finish<NT>(m, pl, c, s, o);
+  w_reset_finish<NT, TK>(m, pl, c, s, o);
 }
 
 /* mid-step state of an env between the substep units of the queued step kernel (w_env_step_q):
@@ -992,10 +994,11 @@ WD void w_store_mid(KModel m, double* __restrict__ mid, int e, const KS& s) {
 #define W_BAIL 0
 #define W_DONE 1
 #define W_PAUSED 2
-template <int NT, class KS>
+template <int NT, int TK = -1, class KS>
 WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
                        const double* __restrict__ actions, int adim, KS& s, WOut& o, int sub_begin = 0,
                        int sub_end = 1 << 30, const double* __restrict__ mid = nullptr) {
+  const int TASK = TK >= 0 ? TK : c.task; /* TK >= 0: kernel specialised for one task at compile time */
   const int tid = w_lane();
   WT_START();
   w_load<NT>(m, c, st, e, s, o);
@@ -1017,10 +1020,10 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   WT(24);
   if (tid == 0 && sub_begin == 0) {
     double ctrl[K_NU];
-    if (c.task == UR3E_TASK_GYM_V2 || c.task == UR3E_TASK_TRAJ_L || c.task == UR3E_TASK_GYM_V0 ||
-        c.task == UR3E_TASK_IMIT_INDIRECT) {
+    if (TASK == UR3E_TASK_GYM_V2 || TASK == UR3E_TASK_TRAJ_L || TASK == UR3E_TASK_GYM_V0 ||
+        TASK == UR3E_TASK_IMIT_INDIRECT) {
       double traj[7];
-      if (c.task != UR3E_TASK_TRAJ_L) { /* [x, y, z] + fixed rotvec + grip */
+      if (TASK != UR3E_TASK_TRAJ_L) { /* [x, y, z] + fixed rotvec + grip */
         traj[0] = o.a[0]; traj[1] = o.a[1]; traj[2] = o.a[2];
         traj[3] = -1.209; traj[4] = -1.209; traj[5] = 1.209;
         traj[6] = o.a[3];
@@ -1031,9 +1034,9 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       k_pid_task_ctrl(traj, o.carry, s.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
       for (int k = 0; k < 6; k++) ctrl[k] = out[k];
       if (m->nu > 6) ctrl[6] = out[6];
-    } else if (c.task == UR3E_TASK_MOVE_L) {
+    } else if (TASK == UR3E_TASK_MOVE_L) {
       k_move_l_ctrl(m, o.a, o.carry, s.qpos, s.qvel, c.gains, ctrl);
-    } else if (c.task == UR3E_TASK_MOVE_J) {
+    } else if (TASK == UR3E_TASK_MOVE_J) {
       for (int k = 0; k < 6; k++) {
         double q = s.qpos[k];
         double delta = o.a[k] - q;
@@ -1057,7 +1060,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       if (k < m->nu) s.ctrl[k] = ctrl[k];
   }
   SYNC();
-  const int fs = (k_is_gym(c.task) || c.task == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  const int fs = (k_is_gym(TASK) || TASK == UR3E_TASK_CTRL) ? c.frame_skip : 1;
   /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
   int sub = sub_begin, retried = 0, resetting = 0;
   w_step_pre<NT>(m, s);
@@ -1080,7 +1083,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     w_forward<NT>(m, pl, s);
     if (KS::BAIL && s.ovf) return W_BAIL;
     if (resetting) {
-      w_reset_finish<NT>(m, pl, c, s, o);
+      w_reset_finish<NT, TK>(m, pl, c, s, o);
       return W_DONE;
     }
     if (!retried && w_step_badacc<NT>(m, s)) {
@@ -1097,7 +1100,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     w_make_carry<NT>(m, pl, s, o.carry);
     SYNC();
     WT(25);
-    if (!k_is_gym(c.task)) {
+    if (!k_is_gym(TASK)) {
       if (tid == 0) {
         o.t += 1; o.ep_len += 1;
         if (c.obs_sites) w_obs_v2(m, s, o.obs);
@@ -1105,13 +1108,13 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       SYNC();
       return W_DONE;
     }
-    if (tid == 0 && c.task != UR3E_TASK_GYM_V2) {
+    if (tid == 0 && TASK != UR3E_TASK_GYM_V2) {
       /* ur3e-v0 / imitation envs: truncation tests t before the increment (ur3e_env.py:152-163,
          imitation_env_indirect.py:96-101, imitation_env_direct.py:98-103) */
-      w_task_obs(m, s, c.task, o.obs);
+      w_task_obs(m, s, TASK, o.obs);
       double r = -1.0;
       int term = 0;
-      if (c.task == UR3E_TASK_GYM_V0) {
+      if (TASK == UR3E_TASK_GYM_V0) {
         const int sc = w_self_collision(m, s);
         r = k_reward_v0(m, o.obs, o.a, sc, w_table_collision(m, s));
         term = k_termination_v0(m, o.obs, sc);
@@ -1144,7 +1147,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     SYNC();
     WT(26);
     if ((o.term || o.trunc) && c.auto_reset) {
-      for (int k = tid; k < k_obs_dim(c.task); k += NT) o.tobs[k] = o.obs[k];
+      for (int k = tid; k < k_obs_dim(TASK); k += NT) o.tobs[k] = o.obs[k];
       if (tid == 0) o.did_reset = 1;
       SYNC();
       w_reset_prep<NT>(m, c, e, s, o);
@@ -1195,7 +1198,7 @@ KD int k_xcd_env(int b, int n) {
   return (b & 7) * (n >> 3) + (b >> 3);
 }
 
-template <int NT, class KS>
+template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                   KConfig c, KState st, const double* __restrict__ actions, int adim,
                                                   double* __restrict__ obs_out, double* __restrict__ rew_out,
@@ -1212,7 +1215,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   WT_INIT();
-  if (w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
+  if (w_env_step_body<NT, TK>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
     if (threadIdx.x == 0) {
       /* each env is appended at most once per step and the fallback kernel re-zeroes the counter,
          so the slot is < n; the bound check keeps a corrupted counter from writing out of range */
@@ -1222,7 +1225,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
     WT_FLUSH();
     return;
   }
-  w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+  w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
   WT(27);
   WT_FLUSH();
 #ifdef UR3E_WAVE_TRACE
@@ -1255,7 +1258,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
 #define W_NQUEUE 8 /* one unit queue per XCD (workgroup b serves queue b % 8: speed only) */
 KD int w_flag_poll(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-template <int NT, class KS>
+template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_model_t* __restrict__ m,
                                                                   const KPlan* __restrict__ pl, KConfig c, KState st,
                                                                   const double* __restrict__ actions, int adim,
@@ -1316,7 +1319,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* payload loads are sc1: keep them below */
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
-    const int r = w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o, sub, sub + 1, mid);
+    const int r = w_env_step_body<NT, TK>(m, pl, c, st, e, actions, adim, s, o, sub, sub + 1, mid);
     if (r == W_BAIL) {
       if (tid == 0) {
         /* the full-capacity tier recomputes the whole env-step from the committed state */
@@ -1334,7 +1337,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
         if (old == bailed) atomicExch(flags + e, bailed); /* a consumer gave up and claimed the env */
       }
     } else {
-      w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+      w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
     }
     SYNC();
   }
@@ -1671,7 +1674,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.sensors = cfg->sensors != 0;
   KPlan plan;
   build_plan(model, &plan);
-  b->main_tree = model->nv == UR3E_MAIN_NV;
+  b->main_tree = model->nv == UR3E_MAIN_NV && plan.max_jntnum <= 1;
   for (int i = 0; i < model->nv && b->main_tree; i++)
     if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) b->main_tree = 0;
   for (int k = 0; k < 12; k++) {
@@ -1862,11 +1865,28 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
                          nullptr, nullptr);
       HIPCHK(hipEventRecord(b->ev_join, b->side));
     }
-    if (b->queued) /* substep work queue (w_env_step_q) */
-      hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
-                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid);
-    else if (b->main_tree) /* main.xml: dof count and tree specialised at compile time */
+    /* main.xml: dof count and tree specialised at compile time; the gym ur3e-v2 and scripted
+       move_l_mug tasks also get kernels specialised for their task (the other tasks' controller and
+       epilogue code folds away, which keeps the register budget for the task that runs) */
+    if (b->queued) { /* substep work queue (w_env_step_q) */
+      if (task == UR3E_TASK_GYM_V2)
+        hipLaunchKernelGGL((w_env_step_q<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), 0, st,
+                           b->d_model, b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated,
+                           d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
+                           b->d_mid);
+      else
+        hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+                           b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                           d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid);
+    } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
+      hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), 0, st, b->d_model,
+                         b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+    } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
+      hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), 0, st, b->d_model,
+                         b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+    } else if (b->main_tree)
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
                          b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_ctl);

@@ -151,68 +151,77 @@ KD void k_mul_quat(double res[4], const double a[4], const double b[4]) {
   res[0] = r0; res[1] = r1; res[2] = r2; res[3] = r3;
 }
 
+/* The small quaternion helpers below keep MuJoCo's special cases (zero vector, identity quaternion,
+   degenerate norm, zero angle) as selects instead of branches: the values are identical, and arrays
+   written on both sides of a branch no longer end up in private (scratch) memory. */
 KD void k_rot_vec_quat(double res[3], const double v[3], const double q[4]) {
-  if (v[0] == 0 && v[1] == 0 && v[2] == 0) {
-    res[0] = res[1] = res[2] = 0;
-  } else if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
-    res[0] = v[0]; res[1] = v[1]; res[2] = v[2];
-  } else {
-    double t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
-    double t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
-    double t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
-    double r0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
-    double r1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
-    double r2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
-    res[0] = r0; res[1] = r1; res[2] = r2;
-  }
+  const double v0 = v[0], v1 = v[1], v2 = v[2];
+  const bool vz = v0 == 0 && v1 == 0 && v2 == 0;
+  const bool qi = q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0;
+  double t0 = q[0] * v0 + q[2] * v2 - q[3] * v1;
+  double t1 = q[0] * v1 + q[3] * v0 - q[1] * v2;
+  double t2 = q[0] * v2 + q[1] * v1 - q[2] * v0;
+  double r0 = v0 + 2 * (q[2] * t2 - q[3] * t1);
+  double r1 = v1 + 2 * (q[3] * t0 - q[1] * t2);
+  double r2 = v2 + 2 * (q[1] * t1 - q[2] * t0);
+  res[0] = vz ? 0.0 : (qi ? v0 : r0);
+  res[1] = vz ? 0.0 : (qi ? v1 : r1);
+  res[2] = vz ? 0.0 : (qi ? v2 : r2);
 }
 
 KD void k_quat2mat(double r[9], const double q[4]) {
-  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
-    r[0] = 1; r[1] = 0; r[2] = 0; r[3] = 0; r[4] = 1; r[5] = 0; r[6] = 0; r[7] = 0; r[8] = 1;
-    return;
-  }
+  const bool qi = q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0;
   double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
   double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
   double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
-  r[0] = q00 + q11 - q22 - q33;
-  r[4] = q00 - q11 + q22 - q33;
-  r[8] = q00 - q11 - q22 + q33;
-  r[1] = 2 * (q12 - q03);
-  r[2] = 2 * (q13 + q02);
-  r[3] = 2 * (q12 + q03);
-  r[5] = 2 * (q23 - q01);
-  r[6] = 2 * (q13 - q02);
-  r[7] = 2 * (q23 + q01);
+  const double m0 = q00 + q11 - q22 - q33;
+  const double m4 = q00 - q11 + q22 - q33;
+  const double m8 = q00 - q11 - q22 + q33;
+  const double m1 = 2 * (q12 - q03);
+  const double m2 = 2 * (q13 + q02);
+  const double m3 = 2 * (q12 + q03);
+  const double m5 = 2 * (q23 - q01);
+  const double m6 = 2 * (q13 - q02);
+  const double m7 = 2 * (q23 + q01);
+  r[0] = qi ? 1.0 : m0; r[1] = qi ? 0.0 : m1; r[2] = qi ? 0.0 : m2;
+  r[3] = qi ? 0.0 : m3; r[4] = qi ? 1.0 : m4; r[5] = qi ? 0.0 : m5;
+  r[6] = qi ? 0.0 : m6; r[7] = qi ? 0.0 : m7; r[8] = qi ? 1.0 : m8;
 }
 
 KD void k_normalize4(double q[4]) {
-  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  if (n < K_MINVAL) {
-    q[0] = 1; q[1] = q[2] = q[3] = 0;
-  } else if (fabs(n - 1.0) > K_MINVAL) {
-    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
-  }
+  const double a = q[0], b = q[1], c = q[2], d = q[3];
+  double n = sqrt(a * a + b * b + c * c + d * d);
+  const bool tiny = n < K_MINVAL;
+  double ra = a, rb = b, rc = c, rd = d;
+  /* the divisions stay behind a branch (skipped when no lane needs them: an already unit
+     quaternion, the common case); only scalars are assigned in it */
+  if (!tiny && fabs(n - 1.0) > K_MINVAL) { ra = a / n; rb = b / n; rc = c / n; rd = d / n; }
+  q[0] = tiny ? 1.0 : ra;
+  q[1] = tiny ? 0.0 : rb;
+  q[2] = tiny ? 0.0 : rc;
+  q[3] = tiny ? 0.0 : rd;
 }
 
 KD double k_normalize3(double v[3]) {
-  double n = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-  if (n < K_MINVAL) {
-    v[0] = 1; v[1] = 0; v[2] = 0;
-    return 0;
-  }
-  v[0] /= n; v[1] /= n; v[2] /= n;
-  return n;
+  const double a = v[0], b = v[1], c = v[2];
+  double n = sqrt(a * a + b * b + c * c);
+  const bool tiny = n < K_MINVAL;
+  double ra = 1, rb = 0, rc = 0;
+  if (!tiny) { ra = a / n; rb = b / n; rc = c / n; }
+  v[0] = tiny ? 1.0 : ra;
+  v[1] = tiny ? 0.0 : rb;
+  v[2] = tiny ? 0.0 : rc;
+  return tiny ? 0.0 : n;
 }
 
 KD void k_axis_angle_quat(double q[4], const double axis[3], double angle) {
-  if (angle == 0) {
-    q[0] = 1; q[1] = q[2] = q[3] = 0;
-    return;
+  double c = 1, x = 0, y = 0, z = 0;
+  if (angle != 0) {
+    double s = ur3e_sin(angle * 0.5);
+    c = ur3e_cos(angle * 0.5);
+    x = axis[0] * s; y = axis[1] * s; z = axis[2] * s;
   }
-  double s = ur3e_sin(angle * 0.5);
-  q[0] = ur3e_cos(angle * 0.5);
-  q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+  q[0] = c; q[1] = x; q[2] = y; q[3] = z;
 }
 
 KD void k_mat_vec3(double r[3], const double m[9], const double v[3]) {

@@ -1887,7 +1887,10 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   static_assert(!KS::OVERLAY || REG, "the overlaid layout is only valid for the 64-lane register path");
   WT(23);
   if constexpr (REG) {
-    if (pl->max_jntnum <= 1) r_kinematics(m, pl, s);
+    /* the main.xml-specialised kernels only run on models with <= 1 joint per body (host check), so
+       the general per-level pass is not compiled into them */
+    if constexpr (KS::STATIC_TREE) r_kinematics(m, pl, s);
+    else if (pl->max_jntnum <= 1) r_kinematics(m, pl, s);
     else w_kinematics<NT>(m, pl, s);
   } else {
     w_kinematics<NT>(m, pl, s);
