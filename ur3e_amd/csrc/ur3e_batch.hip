@@ -943,7 +943,9 @@ WD void w_reset_env(KModel m, const KPlan* __restrict__ pl, const KConfig& c, in
 #define W_MID_WARM (K_NQ + K_NV)
 #define W_MID_CTRL (K_NQ + 2 * K_NV)
 #define W_MID_NWARN (K_NQ + 2 * K_NV + K_NU)
-#define W_MID (((W_MID_NWARN + 1) + 7) / 8 * 8)
+/* records padded to whole 128-B lines (80 doubles): no line is shared by two envs, and one store
+   instruction of the storing wave writes every line of the record whole */
+#define W_MID (((W_MID_NWARN + 1) + 15) / 16 * 16)
 
 /* hand-off words go write-through / L1-bypassing (sc1) at agent scope, so neither side needs a
    cache-maintenance fence (the MI355X publish/consume recipe R1: payload stores sc1 and drained
@@ -952,9 +954,6 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 KD void w_put_sc1(double* p, double v) {
   __hip_atomic_store((gu64_t*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
-}
-KD double w_get_sc1(const double* p) {
-  return __builtin_bit_cast(double, __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 template <int NT, class KS>
@@ -1007,14 +1006,30 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   SYNC();
   if (sub_begin > 0) {
     /* resume: the state after the previous unit's substeps, and the ctrl it applied */
+    /* one 16-byte sc1 load per lane (the record's doubles 2 tid, 2 tid + 1), scattered to LDS */
     const double* p = mid + (size_t)e * W_MID;
-    for (int k = tid; k < m->nq; k += NT) s.qpos[k] = w_get_sc1(p + W_MID_QPOS + k);
-    for (int k = tid; k < m->nv; k += NT) {
-      s.qvel[k] = w_get_sc1(p + W_MID_QVEL + k);
-      s.warm[k] = w_get_sc1(p + W_MID_WARM + k);
+    if (tid < W_MID / 2) {
+      __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, W_MID * 8, 0x00020000);
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+      const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 0, 16);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int k = 2 * tid + h;
+        const double x = __builtin_bit_cast(
+            double, (unsigned long long)w[2 * h] | ((unsigned long long)w[2 * h + 1] << 32));
+        if (k < W_MID_QVEL) {
+          if (k < m->nq) s.qpos[k] = x;
+        } else if (k < W_MID_WARM) {
+          if (k - W_MID_QVEL < m->nv) s.qvel[k - W_MID_QVEL] = x;
+        } else if (k < W_MID_CTRL) {
+          if (k - W_MID_WARM < m->nv) s.warm[k - W_MID_WARM] = x;
+        } else if (k < W_MID_NWARN) {
+          if (k - W_MID_CTRL < m->nu) s.ctrl[k - W_MID_CTRL] = x;
+        } else if (k == W_MID_NWARN) {
+          s.nwarn = (int)x;
+        }
+      }
     }
-    for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = w_get_sc1(p + W_MID_CTRL + k);
-    if (tid == 0) s.nwarn = (int)w_get_sc1(p + W_MID_NWARN);
     SYNC();
   }
   WT(24);
