@@ -85,8 +85,9 @@ KD void k_quat_from_rotvec(const double rv[3], double q[4]) {
 }
 
 KD void k_rotvec_from_quat(const double qin[4], double rv[3]) {
-  double q[4] = {qin[0], qin[1], qin[2], qin[3]};
-  if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+  /* the sign flip as selects: a conditionally rewritten array would live in scratch */
+  const bool neg = qin[3] < 0;
+  double q[4] = {neg ? -qin[0] : qin[0], neg ? -qin[1] : qin[1], neg ? -qin[2] : qin[2], neg ? -qin[3] : qin[3]};
   double ang = 2 * ur3e_atan2(sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]), q[3]);
   double sc;
   if (ang <= 1e-3) {
@@ -833,6 +834,9 @@ struct WOut {
   double r, ep_return;
   int term, trunc, t, ep_len, did_reset;
   unsigned int episode;
+  /* the env index, parked in LDS for the uses after the forward passes (auto-reset, queue hand-off,
+     commit): kept in a register across the step it and the addresses derived from it were spilled */
+  int e;
 };
 
 template <int NT, class KS>
@@ -851,7 +855,7 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
     if constexpr (KS::OVERLAY) s.np_lanes = c.np_lanes;
     else s.sens = c.sensors;
     o.t = st.t[e]; o.ep_len = st.ep_len[e]; o.ep_return = st.ep_return[e]; o.episode = st.episode[e];
-    o.did_reset = 0; o.term = 0; o.trunc = 0; o.r = 0;
+    o.did_reset = 0; o.term = 0; o.trunc = 0; o.r = 0; o.e = e;
   }
 }
 
@@ -1165,7 +1169,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       for (int k = tid; k < k_obs_dim(TASK); k += NT) o.tobs[k] = o.obs[k];
       if (tid == 0) o.did_reset = 1;
       SYNC();
-      w_reset_prep<NT>(m, c, e, s, o);
+      w_reset_prep<NT>(m, c, __builtin_amdgcn_readfirstlane(o.e), s, o);
       resetting = 1;
       continue;
     }
@@ -1306,27 +1310,27 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     const int u = __builtin_amdgcn_readfirstlane(s_u);
     if (u >= total) break;
     const int sub = u / nper;
-    const int e = q * nper + (u - sub * nper);
-    if (st.route && __builtin_amdgcn_readfirstlane(st.route[e])) continue; /* stepped by the grasp tier */
+    const int e0 = q * nper + (u - sub * nper);
+    if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
     if (sub > 0) {
       if (tid == 0) {
         const int want = (E << 4) | sub;
-        int f = w_flag_poll(flags + e);
+        int f = w_flag_poll(flags + e0);
         unsigned int spins = 0;
         while (f != want && f != bailed) {
           if (++spins > W_SPIN_LIMIT) {
-            const int old = atomicExch(flags + e, bailed);
+            const int old = atomicExch(flags + e0, bailed);
             if (old == want) {
               f = want; /* released while we gave up: keep going (and keep the flag final) */
-              atomicExch(flags + e, want);
+              atomicExch(flags + e0, want);
             } else {
               f = bailed;
-              if (old != bailed) ovf_list[min(atomicAdd(ovf_ctl, 1), n - 1)] = e;
+              if (old != bailed) ovf_list[min(atomicAdd(ovf_ctl, 1), n - 1)] = e0;
             }
             break;
           }
           __builtin_amdgcn_s_sleep(2);
-          f = w_flag_poll(flags + e);
+          f = w_flag_poll(flags + e0);
         }
         s_flag = f;
       }
@@ -1334,7 +1338,9 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* payload loads are sc1: keep them below */
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
-    const int r = w_env_step_body<NT, TK>(m, pl, c, st, e, actions, adim, s, o, sub, sub + 1, mid);
+    const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, sub, sub + 1, mid);
+    const int r = __builtin_amdgcn_readfirstlane(r0);
+    const int e = __builtin_amdgcn_readfirstlane(o.e); /* = e0, reloaded from LDS (see WOut::e) */
     if (r == W_BAIL) {
       if (tid == 0) {
         /* the full-capacity tier recomputes the whole env-step from the committed state */
