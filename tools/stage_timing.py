@@ -10,8 +10,8 @@ REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, REPO)
 LIB = os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_timing.so")
 if not os.path.exists(LIB):
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-                    "-shared", "-Wno-unused-result", "-DUR3E_STAGE_TIMING", "-DW_SMALL_MAXCON=9", "-o", LIB,
+    from ur3e_amd import _build  # same flags as the product library (incl. -disable-machine-licm)
+    subprocess.run([_build.HIPCC] + _build.FLAGS + ["-DUR3E_STAGE_TIMING", "-DW_SMALL_MAXCON=9", "-o", LIB,
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip"),
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_vecnorm.hip")], check=True)
 os.environ["UR3E_LIB"] = LIB

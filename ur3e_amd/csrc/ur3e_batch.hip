@@ -1312,6 +1312,9 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     const int sub = u / nper;
     const int e0 = q * nper + (u - sub * nper);
     if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
+#ifdef UR3E_WAVE_TRACE
+    if (tid == 0 && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (sub > 0) {
       if (tid == 0) {
         const int want = (E << 4) | sub;
@@ -1338,6 +1341,9 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* payload loads are sc1: keep them below */
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
+#ifdef UR3E_WAVE_TRACE
+    if (tid == 0 && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, sub, sub + 1, mid);
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const int e = __builtin_amdgcn_readfirstlane(o.e); /* = e0, reloaded from LDS (see WOut::e) */
@@ -1361,6 +1367,15 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
     }
     SYNC();
+#ifdef UR3E_WAVE_TRACE
+    /* per unit (sub * n + e): pulled, flag acquired, finished (s_memrealtime), workgroup | XCC << 32 */
+    if (tid == 0 && sub * n + e < UR3E_WAVE_TRACE_MAX) {
+      unsigned long long* tr = ur3e_wave_trace[sub * n + e];
+      tr[2] = __builtin_amdgcn_s_memrealtime();
+      tr[3] = (unsigned long long)blockIdx.x |
+              ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+    }
+#endif
   }
   if (tid == 0) {
     __threadfence();

@@ -919,41 +919,77 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  /* MuJoCo's per-body recurrence (mj_kinematics), split so that only its true dependency chain runs
+     level by level:
+       1. orientation chain: q1 = parent xquat * body_quat, q2 = q1 * qloc, xquat = normalize(q2);
+       2. every body at once: xmat = quat2mat(xquat), the joint axis and the two joint-position
+          rotations (by q1 and by q2), and tv = parent xmat * body_pos;
+       3. position chain: xpos = ((parent xpos + tv) + xanchor offset) - rotated joint pos.
+     Every value is the same expression of the same operands as in the one-pass recurrence (only
+     its place in time moves), so the results are bit-identical; the 13-level chain now carries
+     ~100 instructions per level instead of ~550. */
+  const bool isfree = jn == 1 && jt == UR3E_JNT_FREE;
+  const bool hinge = depth > 0 && jn == 1 && !isfree;
+  double q1[4] = {1, 0, 0, 0}, q2[4] = {1, 0, 0, 0}, xq[4] = {1, 0, 0, 0};
   for (int lvl = 1; lvl <= nlevel; lvl++) {
     if (depth == lvl) {
-      double xpos[3], xquat[4];
-      if (jn == 1 && jt == UR3E_JNT_FREE) {
-        xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
-        xquat[0] = s.qpos[qa + 3]; xquat[1] = s.qpos[qa + 4]; xquat[2] = s.qpos[qa + 5]; xquat[3] = s.qpos[qa + 6];
-        k_normalize4(xquat);
-        s.xanchor[jf][0] = xpos[0]; s.xanchor[jf][1] = xpos[1]; s.xanchor[jf][2] = xpos[2];
-        s.xaxis[jf][0] = 0; s.xaxis[jf][1] = 0; s.xaxis[jf][2] = 1;
+      if (isfree) {
+        xq[0] = s.qpos[qa + 3]; xq[1] = s.qpos[qa + 4]; xq[2] = s.qpos[qa + 5]; xq[3] = s.qpos[qa + 6];
       } else {
-        double pm[9], pp[3], pq[4];
-        for (int c = 0; c < 9; c++) pm[c] = s.xmat[pid][c];
-        for (int c = 0; c < 3; c++) pp[c] = s.xpos[pid][c];
+        double pq[4];
         for (int c = 0; c < 4; c++) pq[c] = s.xquat[pid][c];
-        double tv[3];
-        k_mat_vec3(tv, pm, bpos);
-        xpos[0] = pp[0] + tv[0]; xpos[1] = pp[1] + tv[1]; xpos[2] = pp[2] + tv[2];
-        k_mul_quat(xquat, pq, bquat);
+        k_mul_quat(q1, pq, bquat);
+        if (jn == 1) k_mul_quat(q2, q1, ql);
+        else for (int c = 0; c < 4; c++) q2[c] = q1[c];
+        for (int c = 0; c < 4; c++) xq[c] = q2[c];
+      }
+      k_normalize4(xq);
+      for (int c = 0; c < 4; c++) s.xquat[lane][c] = xq[c];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  /* 2. orientation-only terms of every body */
+  double ra[3] = {0, 0, 0}, vec[3] = {0, 0, 0};
+  if (depth > 0) {
+    double xm[9];
+    k_quat2mat(xm, xq);
+    for (int c = 0; c < 9; c++) s.xmat[lane][c] = xm[c];
+    if (hinge) {
+      double xaxis[3];
+      k_rot_vec_quat(xaxis, jax, q1);
+      k_rot_vec_quat(ra, jps, q1);
+      k_rot_vec_quat(vec, jps, q2);
+      for (int c = 0; c < 3; c++) s.xaxis[jf][c] = xaxis[c];
+    } else if (isfree) {
+      s.xaxis[jf][0] = 0; s.xaxis[jf][1] = 0; s.xaxis[jf][2] = 1;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  double tv[3] = {0, 0, 0};
+  if (depth > 0 && !isfree) {
+    double pm[9];
+    for (int c = 0; c < 9; c++) pm[c] = s.xmat[pid][c];
+    k_mat_vec3(tv, pm, bpos);
+  }
+  /* 3. position chain */
+  for (int lvl = 1; lvl <= nlevel; lvl++) {
+    if (depth == lvl) {
+      double xpos[3];
+      if (isfree) {
+        xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
+        s.xanchor[jf][0] = xpos[0]; s.xanchor[jf][1] = xpos[1]; s.xanchor[jf][2] = xpos[2];
+      } else {
+        for (int c = 0; c < 3; c++) xpos[c] = s.xpos[pid][c] + tv[c];
         if (jn == 1) {
-          double xaxis[3], xanchor[3], vec[3];
-          k_rot_vec_quat(xaxis, jax, xquat);
-          k_rot_vec_quat(xanchor, jps, xquat);
-          xanchor[0] += xpos[0]; xanchor[1] += xpos[1]; xanchor[2] += xpos[2];
-          k_mul_quat(xquat, xquat, ql);
-          k_rot_vec_quat(vec, jps, xquat);
-          xpos[0] = xanchor[0] - vec[0]; xpos[1] = xanchor[1] - vec[1]; xpos[2] = xanchor[2] - vec[2];
-          for (int c = 0; c < 3; c++) { s.xanchor[jf][c] = xanchor[c]; s.xaxis[jf][c] = xaxis[c]; }
+          double xanchor[3];
+          for (int c = 0; c < 3; c++) xanchor[c] = ra[c] + xpos[c];
+          for (int c = 0; c < 3; c++) xpos[c] = xanchor[c] - vec[c];
+          for (int c = 0; c < 3; c++) s.xanchor[jf][c] = xanchor[c];
         }
       }
-      k_normalize4(xquat);
       for (int c = 0; c < 3; c++) s.xpos[lane][c] = xpos[c];
-      for (int c = 0; c < 4; c++) s.xquat[lane][c] = xquat[c];
-      double xm[9];
-      k_quat2mat(xm, xquat);
-      for (int c = 0; c < 9; c++) s.xmat[lane][c] = xm[c];
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
@@ -1002,47 +1038,58 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  /* Split like r_kinematics: the velocity chain cvel = parent cvel + cdof * qvel runs level by level,
+     then cdof_dot and the acceleration term of every single-dof body are formed at once, then the
+     chain cacc = parent cacc + term.  Same expressions, same operands: bit-identical. */
+  const bool one = bdn == 1 && jt != UR3E_JNT_FREE;
+  double cqv[6], cvp[6] = {0, 0, 0, 0, 0, 0}, tmp[6] = {0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < 6; r++) cqv[r] = cd[r] * qv;
   for (int lvl = 1; lvl <= nlevel; lvl++) {
     if (depth == lvl) {
-      double cv[6], ca[6];
-      for (int k = 0; k < 6; k++) { cv[k] = s.cvel[pid][k]; ca[k] = cacc[pid][k]; }
-      if (bdn == 1 && jt != UR3E_JNT_FREE) {
-        double cdd[6];
-        k_cross_motion(cdd, cv, cd);
-        for (int r = 0; r < 6; r++) cv[r] += cd[r] * qv;
-        for (int r = 0; r < 6; r++) s.cdof_dot[bda][r] = cdd[r];
-        double tmp[6] = {0, 0, 0, 0, 0, 0};
-        for (int r = 0; r < 6; r++) tmp[r] += cdd[r] * qv;
-        for (int r = 0; r < 6; r++) ca[r] = ca[r] + tmp[r];
+      double cv[6];
+      for (int k = 0; k < 6; k++) cv[k] = s.cvel[pid][k];
+      if (one) {
+        for (int r = 0; r < 6; r++) { cvp[r] = cv[r]; cv[r] += cqv[r]; }
       } else {
-        /* general body (free joint, several dofs): w_com_vel then the cacc sum */
+        /* general body (free joint, several dofs, none): w_com_vel, and its cacc term */
         for (int j = 0; j < bdn; j++) {
           int dof = bda + j;
           int jtj = m->jnt_type[m->dof_jntid[dof]];
           if (jtj == UR3E_JNT_FREE) {
             for (int k = 0; k < 3; k++)
               for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
-            double tmp[6] = {0, 0, 0, 0, 0, 0};
+            double tq[6] = {0, 0, 0, 0, 0, 0};
             for (int k = 0; k < 3; k++)
-              for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
-            for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+              for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+            for (int r = 0; r < 6; r++) cv[r] += tq[r];
             for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
-            for (int r = 0; r < 6; r++) tmp[r] = 0;
+            for (int r = 0; r < 6; r++) tq[r] = 0;
             for (int k = 3; k < 6; k++)
-              for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
-            for (int r = 0; r < 6; r++) cv[r] += tmp[r];
+              for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+            for (int r = 0; r < 6; r++) cv[r] += tq[r];
             j += 5;
           } else {
             k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
             for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
           }
         }
-        double tmp[6] = {0, 0, 0, 0, 0, 0};
         for (int j = 0; j < bdn; j++)
           for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
-        for (int r = 0; r < 6; r++) ca[r] = ca[r] + tmp[r];
       }
-      for (int k = 0; k < 6; k++) { s.cvel[lane][k] = cv[k]; cacc[lane][k] = ca[k]; }
+      for (int k = 0; k < 6; k++) s.cvel[lane][k] = cv[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (depth > 0 && one) {
+    double cdd[6];
+    k_cross_motion(cdd, cvp, cd);
+    for (int r = 0; r < 6; r++) s.cdof_dot[bda][r] = cdd[r];
+    for (int r = 0; r < 6; r++) tmp[r] += cdd[r] * qv;
+  }
+  for (int lvl = 1; lvl <= nlevel; lvl++) {
+    if (depth == lvl) {
+      for (int k = 0; k < 6; k++) cacc[lane][k] = cacc[pid][k] + tmp[k];
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
