@@ -36,15 +36,17 @@ if __name__ == "__main__":
         torch.cuda.synchronize()
         print("warm-up step", i, flush=True)
     nu = n * fs
+    nrow = 8192 + 2048  # units, then one row per workgroup (start, exit)
     if product:
         print("product library: warm-up steps ran", flush=True)
         sys.exit(0)
-    buf = np.zeros((nu, 4), dtype=np.uint64)
+    full = np.zeros((nrow, 4), dtype=np.uint64)
+    raws = []
     for i in range(steps):
-        buf[:] = 0
         b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
         torch.cuda.synchronize()
-        assert L.ur3e_debug_wave_trace(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), nu) == 0
+        assert L.ur3e_debug_wave_trace(full.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), nrow) == 0
+        buf = full[:nu]
         ok = buf[:, 2] > 0
         tp, tr, te = (buf[:, k].astype(np.int64) for k in range(3))
         base = tp[ok].min()
@@ -74,4 +76,8 @@ if __name__ == "__main__":
                  slot_end_p10_p50_p90_us=[round(float(np.percentile(last_end, q)), 1) for q in (10, 50, 90)],
                  units_per_slot=[int(x) for x in np.percentile(np.bincount(wg[ok]), [0, 50, 100])])
         print(json.dumps(r), flush=True)
+        raws.append(full.copy())
+    out = os.environ.get("UR3E_TRACE_OUT")
+    if out:
+        np.savez_compressed(out, units=np.stack(raws), n=n, fs=fs)
     b.close()

@@ -1304,16 +1304,30 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
      VGPRs across the step they would be spilled (the kernel is at its 256-register budget) */
   const int E = __builtin_amdgcn_readfirstlane(s_epoch);
   const int bailed = (E << 4) | W_FLAG_BAILED;
+#ifdef UR3E_WAVE_TRACE
+  /* per workgroup (row 8192 + blockIdx): started, exited */
+  if (8192 + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[8192 + blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  /* the first unit of every workgroup is static (its rank in its queue; the counters start at the
+     number of workgroups per queue): 2,048 workgroups contending for eight counters at once cost
+     ~10 us of the launch */
+  int first = 1;
   for (;;) {
-    if (tid == 0) s_u = atomicAdd(qctl + q, 1);
-    SYNC();
-    const int u = __builtin_amdgcn_readfirstlane(s_u);
+    int u;
+    if (first) {
+      u = (int)blockIdx.x / nq;
+      first = 0;
+    } else {
+      if (tid == 0) s_u = atomicAdd(qctl + q, 1);
+      SYNC();
+      u = __builtin_amdgcn_readfirstlane(s_u);
+    }
     if (u >= total) break;
     const int sub = u / nper;
     const int e0 = q * nper + (u - sub * nper);
     if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
-    if (tid == 0 && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
+    if (sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime(); /* every lane, same word: no exec-masked region */
 #endif
     if (sub > 0) {
       if (tid == 0) {
@@ -1342,7 +1356,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
 #ifdef UR3E_WAVE_TRACE
-    if (tid == 0 && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
+    if (sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime(); /* every lane, same word: no exec-masked region */
 #endif
     const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, sub, sub + 1, mid);
     const int r = __builtin_amdgcn_readfirstlane(r0);
@@ -1369,7 +1383,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     SYNC();
 #ifdef UR3E_WAVE_TRACE
     /* per unit (sub * n + e): pulled, flag acquired, finished (s_memrealtime), workgroup | XCC << 32 */
-    if (tid == 0 && sub * n + e < UR3E_WAVE_TRACE_MAX) {
+    if (sub * n + e < UR3E_WAVE_TRACE_MAX) {
       unsigned long long* tr = ur3e_wave_trace[sub * n + e];
       tr[2] = __builtin_amdgcn_s_memrealtime();
       tr[3] = (unsigned long long)blockIdx.x |
@@ -1377,10 +1391,13 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     }
 #endif
   }
+#ifdef UR3E_WAVE_TRACE
+  if (8192 + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[8192 + blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (tid == 0) {
     __threadfence();
     if (atomicAdd(qctl + W_NQUEUE, 1) == (int)gridDim.x - 1) {
-      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl + k, 0);
+      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl + k, k < nq ? (int)gridDim.x / nq : 0);
       atomicExch(qctl + W_NQUEUE, 0);
       atomicExch(qctl + W_NQUEUE + 1, (E + 1) & 0x7ffffff);
     }
@@ -1807,6 +1824,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     if (!(n_envs & 7)) b->q_grid = b->q_grid / W_NQUEUE * W_NQUEUE;
     if (b->q_grid < W_NQUEUE) b->q_grid = (n_envs & 7) ? (b->q_grid < 1 ? 1 : b->q_grid) : W_NQUEUE;
     int qinit[W_NQUEUE + 2] = {0};
+    /* each queue's counter starts past the workgroups' static first units (w_env_step_q) */
+    const int nq = (n_envs & 7) ? 1 : W_NQUEUE;
+    for (int k = 0; k < nq; k++) qinit[k] = b->q_grid / nq;
     qinit[W_NQUEUE + 1] = 1; /* epoch */
     HIPCHK(hipMalloc(&b->d_qctl, sizeof(qinit)));
     HIPCHK(hipMemcpy(b->d_qctl, qinit, sizeof(qinit), hipMemcpyHostToDevice));
