@@ -392,11 +392,20 @@ struct KState {
      grasp tier concurrently with it.  Routing only picks the tier; every tier gives the same result. */
   unsigned char* hint;
   unsigned char* route;
+  /* host-mapped word: the number of envs the last route snapshot routed (written by the snapshotting
+     workgroup, read by the host without a sync to decide whether the next steps need the pre-pass) */
+  int* routed_host;
 };
 /* an env whose last forward had more contacts or constraint rows than these runs its next step in
    the grasp tier (the compact tier holds 10 contacts / 44 rows; the margin covers the contacts and
    joint-limit rows one step can add) */
 #define W_ROUTE_NCON 8
+/* host-side routing decision (ur3e_batch_step): run-ahead bound and how long routing stays on after
+   the host last saw a routed env */
+#define W_AHEAD 16
+#define W_ROUTE_HOLD 64
+/* grasp-tier workgroups for the compact tier's bails while routing is off (bails are rare then) */
+#define W_GRASP_IDLE_GRID 128
 #define W_ROUTE_NEFC 36
 
 struct KConfig {
@@ -1432,13 +1441,28 @@ __global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __r
        envs for its grasp-tier pre-pass (the order of the list does not matter: envs are independent) */
     if (threadIdx.x == 0) s_cnt = 0;
     SYNC();
-    for (int e = threadIdx.x; e < st.n; e += NT) {
+    /* 16 envs per thread and load (4,096 envs: two passes of the workgroup instead of 32 dependent
+       byte loads per thread) */
+    const int n16 = st.n >> 4;
+    for (int c = threadIdx.x; c < n16; c += NT) {
+      const uint4 h = ((const uint4*)st.hint)[c];
+      ((uint4*)st.route)[c] = h;
+      if (h.x | h.y | h.z | h.w) {
+        const unsigned int w[4] = {h.x, h.y, h.z, h.w};
+        for (int k = 0; k < 16; k++)
+          if ((w[k >> 2] >> (8 * (k & 3))) & 0xffu) pred_list[atomicAdd(&s_cnt, 1)] = 16 * c + k;
+      }
+    }
+    for (int e = 16 * n16 + threadIdx.x; e < st.n; e += NT) {
       const unsigned char h = st.hint[e];
       st.route[e] = h;
       if (h) pred_list[atomicAdd(&s_cnt, 1)] = e;
     }
     SYNC();
-    if (threadIdx.x == 0) __hip_atomic_store(pred_ctl, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(pred_ctl, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st.routed_host) __hip_atomic_store(st.routed_host, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     SYNC();
   }
   /* the producer launch has completed, so every workgroup reads the same final count: with an
@@ -1558,6 +1582,7 @@ struct ur3e_batch {
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
   unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier */
   int grasp;       /* the tiers are compact -> grasp (KSG_NV) -> full capacity (main.xml only) */
+  int* h_routed;   /* host-mapped routed-env count of the last route snapshot (KState.routed_host) */
   int g_grid;      /* resident workgroups of the grasp-tier list kernel */
   int* d_ovf2_list; /* envs the grasp tier handed to the full-capacity tier */
   int* d_ovf2_ctl;
@@ -1565,6 +1590,11 @@ struct ur3e_batch {
   int* d_pred_ctl;
   hipStream_t side; /* the grasp-tier pre-pass runs here, concurrently with the compact tier */
   hipEvent_t ev_fork, ev_join;
+  /* bounded run-ahead (grasp tier on): step k waits for step k - W_AHEAD to finish before it enqueues,
+     so the host-mapped routed count it reads is at most W_AHEAD steps old */
+  hipEvent_t ev_ahead[16];
+  long long hstep;      /* steps enqueued outside graph capture */
+  long long last_route; /* hstep at which the host last saw a nonzero routed count */
   int queued;      /* compact tier through the substep work queue (w_env_step_q) */
   int q_grid;      /* resident workgroups of w_env_step_q (occupancy x CUs) */
   int* d_qctl;     /* {next unit per queue [W_NQUEUE], workgroups done, epoch} */
@@ -1776,7 +1806,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->grasp = tiered && b->main_tree;
   b->d_ovf2_list = nullptr; b->d_ovf2_ctl = nullptr; b->g_grid = 0;
   b->d_pred_list = nullptr; b->d_pred_ctl = nullptr; b->side = nullptr;
-  s.hint = nullptr; s.route = nullptr;
+  s.hint = nullptr; s.route = nullptr; s.routed_host = nullptr; b->h_routed = nullptr;
+  b->hstep = 0; b->last_route = -1;
   if (b->grasp) {
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)w_env_step_list<64, KSG_NV>, 64, 0));
@@ -1794,6 +1825,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMemset(s.hint, 0, nd));
     HIPCHK(hipMalloc(&s.route, nd));
     HIPCHK(hipMemset(s.route, 0, nd));
+    HIPCHK(hipHostMalloc((void**)&b->h_routed, sizeof(int), hipHostMallocMapped));
+    *(volatile int*)b->h_routed = 0;
+    HIPCHK(hipHostGetDevicePointer((void**)&s.routed_host, b->h_routed, 0));
     /* high priority: the routed envs are the long ones, so their workgroups should be dispatched
        before the compact tier's fill the CUs */
     int prio_lo = 0, prio_hi = 0;
@@ -1801,6 +1835,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    for (int k = 0; k < 16; k++) HIPCHK(hipEventCreateWithFlags(&b->ev_ahead[k], hipEventDisableTiming));
   }
   /* substep work queue: gym tasks with several substeps per env-step on main.xml's compact tier
      (cfg->schedule 1 keeps one workgroup per env-step) */
@@ -1860,10 +1895,12 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (b->d_pred_ctl) (void)hipFree(b->d_pred_ctl);
   if (b->st.hint) (void)hipFree(b->st.hint);
   if (b->st.route) (void)hipFree(b->st.route);
+  if (b->h_routed) (void)hipHostFree(b->h_routed);
   if (b->side) {
     (void)hipStreamDestroy(b->side);
     (void)hipEventDestroy(b->ev_fork);
     (void)hipEventDestroy(b->ev_join);
+    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev_ahead[k]);
   }
   if (b->d_flags) (void)hipFree(b->d_flags);
   if (b->d_mid) (void)hipFree(b->d_mid);
@@ -1908,9 +1945,30 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
     HIPCHK(hipStreamIsCapturing(st, &cs));
     record = cs == hipStreamCaptureStatusNone;
   }
+  bool capturing = false;
   if (record) HIPCHK(hipEventRecord(b->ev0, st));
   if (b->tiered) {
+    /* the grasp-tier pre-pass runs only while routing is in use: the last route snapshot the host can
+       see (host-mapped, read without a sync, possibly a step or two old) routed some env, or the step
+       is being captured (a graph replays without the host).  Skipped, the compact tier steps every
+       env (routing is off for this step: route = null), and the few that exceed it bail to the grasp
+       tier after it -- the same results either way, routing only moves work between tiers. */
+    KState kst = b->st;
+    bool pre = false;
     if (b->grasp) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      HIPCHK(hipStreamIsCapturing(st, &cs));
+      capturing = cs != hipStreamCaptureStatusNone;
+      if (!capturing) {
+        const int slot = (int)(b->hstep % W_AHEAD);
+        if (b->hstep >= W_AHEAD) HIPCHK(hipEventSynchronize(b->ev_ahead[slot]));
+        if (*(volatile int*)b->h_routed > 0) b->last_route = b->hstep;
+      }
+      /* routing stays on for W_ROUTE_HOLD steps after the last sighting (it comes in bursts: grasps) */
+      pre = capturing || (b->last_route >= 0 && b->hstep - b->last_route < W_ROUTE_HOLD);
+      if (!pre) kst.route = nullptr;
+    }
+    if (pre) {
       /* fork: envs routed by the last step's hints run in the grasp tier on the side stream while
          the compact tier (which skips them) runs here */
       HIPCHK(hipEventRecord(b->ev_fork, st));
@@ -1927,35 +1985,36 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
     if (b->queued) { /* substep work queue (w_env_step_q) */
       if (task == UR3E_TASK_GYM_V2)
         hipLaunchKernelGGL((w_env_step_q<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), 0, st,
-                           b->d_model, b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated,
+                           b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
                            d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
                            b->d_mid);
       else
         hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
-                           b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                           b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                            d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid);
     } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
       hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), 0, st, b->d_model,
-                         b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                          d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
     } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
       hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), 0, st, b->d_model,
-                         b->d_plan, b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                          d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
     } else if (b->main_tree)
       hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
-                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_ctl);
     else
-      hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+      hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, kst,
                          d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
                          b->d_ovf_ctl);
     int grid = b->n < 512 ? b->n : 512;
     if (b->grasp) {
-      HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
+      if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
       /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier, whose
          workgroup 0 also snapshots the routing hints for the next step */
-      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+      const int post_grid = pre || b->g_grid < W_GRASP_IDLE_GRID ? b->g_grid : W_GRASP_IDLE_GRID;
+      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(post_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                          b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
                          nullptr);
@@ -1980,6 +2039,10 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
     hipLaunchKernelGGL(k_env_step, dim3(grid_of(b)), dim3(64), 0, st, b->d_model, b->cfg, b->st, d_actions, adim,
                        d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
   HIPCHK(hipGetLastError());
+  if (b->tiered && b->grasp && !capturing) {
+    HIPCHK(hipEventRecord(b->ev_ahead[b->hstep % W_AHEAD], st));
+    b->hstep++;
+  }
   if (record) {
     HIPCHK(hipEventRecord(b->ev1, st));
     b->timed = 1;
