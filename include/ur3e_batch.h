@@ -5,7 +5,10 @@
  * One handle = N environments resident in HBM on one GPU.  Every pointer
  * argument named d_* is a DEVICE pointer (e.g. a torch tensor's data_ptr() on
  * the same device); `stream` is a hipStream_t (NULL = default stream).  All
- * calls only enqueue work on `stream` and return immediately.  Return value: 0
+ * calls only enqueue work on `stream` and return immediately (one exception:
+ * on main.xml's tiered step, ur3e_batch_step waits for the step enqueued 16
+ * calls earlier to finish, bounding how far the host runs ahead of the GPU;
+ * never inside a graph capture).  Return value: 0
  * on success, a negative UR3E_E* code otherwise; ur3e_last_error() gives a
  * thread-local message.  A handle is not thread-safe.
  *
