@@ -21,7 +21,8 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
          6: "com_vel", 7: "rne+passive+act", 8: "solve_tree(smooth)", 9: "newton init (eval x2-3, grad)",
          10: "H build", 11: "cholesky / (r) backward solve", 12: "hessian_solve / (r) cholesky",
          18: "(r) forward solve", 19: "(r) ls setup + eval(0)", 20: "(r) ls eval (per call)", 13: "line_search tail", 14: "eval+grad (iter)",
-         15: "newton tail", 21: "touch sensors", 22: "badacc check", 16: "euler factor+solve", 17: "integrate", 25: "make_carry", 26: "obs+reward+termination", 27: "commit"}
+         15: "newton tail", 21: "touch sensors", 22: "badacc check", 16: "euler factor+solve", 17: "integrate", 25: "make_carry", 26: "obs+reward+termination", 27: "commit",
+         28: "(count only) block-diagonal Newton directions"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"
@@ -54,7 +55,7 @@ for f in steps:
     f()
 torch.cuda.synchronize()
 L.ur3e_debug_stage_cycles_tier(tier, cyc, calls, 1)
-tot = sum(cyc[k] for k in names)
+tot = sum(cyc[k] for k in names if k != 28)
 units = calls[23] if calls[23] else 1  # forward passes run (substeps + retries + resets)
 print(f"tier {tier}, workload {work}: per-forward cycles (lane 0 view), {n} envs, {K} steps, "
       f"{calls[23]} forward passes in this tier")

@@ -176,6 +176,7 @@ struct KSX<MC, ME, NVC, TREE, true> {
   double eq_p[UR3E_MAXEQ][6];  /* connect anchors p1, p2 in world coordinates */
   double site_vel[2][6];       /* [tcp, handle] mj_objectVelocity (world, [w, v]) */
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
+  int bdiag; /* static tree: no constraint row couples the two dof trees (set by r_mc_rows) */
   int np_lanes; /* survivor lanes per narrowphase chunk (KConfig.np_lanes, <= W_NP_LANES) */
   unsigned long long tlast;
 #ifdef UR3E_STAGE_TIMING

@@ -347,21 +347,45 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
      e = lane + 64 q (q < 4), each accumulating rows in oracle order; then one LDS transpose
      hands row k to lane k for the factorisation */
   constexpr int NQ = (K_NV * (K_NV + 1) / 2 + 63) / 64;
+  /* Block-diagonal case (static tree, s.bdiag: no row couples the two dof trees [0, S) and [S, nv)):
+     the oracle's H has exact +0 in the cross block (M has none there, and every J'DJ term it adds
+     is a skipped zero or +0 + (+-0) = +0), so its dense Cholesky leaves L's cross block +0 and every
+     update a cross entry makes elsewhere subtracts +0 (x - (+0) == x for all x, signed zeros
+     included).  Only the two diagonal blocks are then built (126 of 210 elements for main.xml: two
+     element slots per lane instead of four) and the factorisation skips the cross updates; the
+     triangular solves stay dense. */
+  constexpr int SPLIT = KS::STATIC_TREE ? UR3E_MAIN_SPLIT : 0;
+  const bool bd = SPLIT > 0 && s.bdiag;
+#ifdef UR3E_STAGE_TIMING
+  if (lane == 0 && bd) s.tcnt[28] += 1; /* diagnostic: block-diagonal Newton directions */
+#endif
   const int nel = nv * (nv + 1) / 2;
-  int ek[NQ], ec[NQ];
+  const int nel1 = SPLIT * (SPLIT + 1) / 2;
+  const int nelb = bd ? nel1 + (nv - SPLIT) * (nv - SPLIT + 1) / 2 : nel;
+  const int nqe = (nelb + 63) / 64; /* element slots in use (uniform) */
+  auto tri_row = [](int e) {
+    int k = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    while (k * (k + 1) / 2 > e) k--;
+    while ((k + 1) * (k + 2) / 2 <= e) k++;
+    return k;
+  };
+  int ek[NQ], ec[NQ], ep[NQ];
   bool ev[NQ];
   double hv[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; q++) {
-    int e = lane + 64 * q;
-    ev[q] = e < nel;
-    int k = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-    while (k * (k + 1) / 2 > e) k--;
-    while ((k + 1) * (k + 2) / 2 <= e) k++;
-    if (!ev[q]) k = 0;
-    ek[q] = k;
-    ec[q] = ev[q] ? e - k * (k + 1) / 2 : 0;
-    hv[q] = s.qMp[ev[q] ? e : 0]; /* element e of the packed lower triangle is (ek, ec) */
+    const int e = lane + 64 * q;
+    ev[q] = e < nelb;
+    /* second block (bd): local packed index e - nel1, offset by SPLIT; one triangle-row solve either way */
+    const bool b2 = bd && e >= nel1;
+    const int t = ev[q] ? (b2 ? e - nel1 : e) : 0;
+    const int a = tri_row(t);
+    const int off = b2 ? SPLIT : 0;
+    const int k = off + a, c = off + t - a * (a + 1) / 2;
+    ek[q] = ev[q] ? k : 0;
+    ec[q] = ev[q] ? c : 0;
+    ep[q] = ev[q] ? KTRI(k, c) : 0; /* packed index of element (ek, ec) */
+    hv[q] = s.qMp[ep[q]];
   }
   /* only rows that add to H are visited, in row order (the others add nothing in the oracle):
      quadratic rows and the first row of each cone-state contact; slot h covers rows 64h.. */
@@ -378,34 +402,39 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
     const int ifirst = act ? (int)__builtin_ctzll(act) : 0;
     double njk[NQ], njc[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[rb + ifirst][ek[q]]; njc[q] = s.efc_J[rb + ifirst][ec[q]]; }
+    for (int q = 0; q < NQ; q++)
+      if (q < nqe) { njk[q] = s.efc_J[rb + ifirst][ek[q]]; njc[q] = s.efc_J[rb + ifirst][ec[q]]; }
     while (act) {
       const int i = (int)__builtin_ctzll(act);
       act &= act - 1;
       double jk[NQ], jc[NQ];
 #pragma unroll
-      for (int q = 0; q < NQ; q++) {
-        jk[q] = njk[q]; jc[q] = njc[q];
-        asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
-      }
+      for (int q = 0; q < NQ; q++)
+        if (q < nqe) {
+          jk[q] = njk[q]; jc[q] = njc[q];
+          asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
+        }
       const int inext = act ? (int)__builtin_ctzll(act) : i;
 #pragma unroll
-      for (int q = 0; q < NQ; q++) { njk[q] = s.efc_J[rb + inext][ek[q]]; njc[q] = s.efc_J[rb + inext][ec[q]]; }
+      for (int q = 0; q < NQ; q++)
+        if (q < nqe) { njk[q] = s.efc_J[rb + inext][ek[q]]; njc[q] = s.efc_J[rb + inext][ec[q]]; }
       const int st = rli(w.st, i);
       if (st == ST_QUADRATIC) {
         const double D = rl(w.D, i);
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          const double djr = D * jk[q];
-          double n = hv[q] + djr * jc[q];
-          asm volatile("" : "+v"(n));
-          hv[q] = jk[q] != 0 ? n : hv[q];
-        }
+        for (int q = 0; q < NQ; q++)
+          if (q < nqe) {
+            const double djr = D * jk[q];
+            double n = hv[q] + djr * jc[q];
+            asm volatile("" : "+v"(n));
+            hv[q] = jk[q] != 0 ? n : hv[q];
+          }
       } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
         const int ri = rb + i;
         const double* Hc = s.con_Hc[s.efc_id[ri]];
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
+          if (q >= nqe) continue;
           double t[3];
           for (int j = 0; j < 3; j++) {
             double acc = 0;
@@ -419,15 +448,17 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
       }
     }
   }
-  /* element e = lane + 64 q is packed-triangle index e */
+  /* element slot q of this lane is packed-triangle index ep[q] */
 #pragma unroll
   for (int q = 0; q < NQ; q++)
-    if (ev[q]) s.Hl[lane + 64 * q] = hv[q];
+    if (q < nqe && ev[q]) s.Hl[ep[q]] = hv[q];
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   double h[K_NV];
+  /* block-diagonal: the cross block is the oracle's exact +0 (not stored) */
+  const int cfrom = bd && row >= SPLIT ? SPLIT : 0;
 #pragma unroll
-  for (int c = 0; c < K_NV; c++) h[c] = c <= row ? s.Hl[KTRI(row, c)] : 0.0;
+  for (int c = 0; c < K_NV; c++) h[c] = (c <= row && c >= cfrom) ? s.Hl[KTRI(row, c)] : 0.0;
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   WT(10);
@@ -446,9 +477,11 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
       /* column j to every lane through an LDS slot (broadcast reads, not a readlane per k) */
       double* col = R_SLOT(s, j & 1);
       r_stage(col, h[j]);
+      /* block-diagonal: a first-block column updates second-block entries by -(+0 * +0): skipped */
+      const int kend = bd && j < SPLIT ? SPLIT : nv;
 #pragma unroll
       for (int k = j + 1; k < K_NV; k++) {
-        if (k < nv) {
+        if (k < kend) {
           const double lkj = col[k];
           if (lane >= k) h[k] -= h[j] * lkj;
         }
@@ -1354,6 +1387,8 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   /* ---- 3. impedance, lane = row (w_row_impedance); row lane + 64 h for each row slot ---- */
+  constexpr int SPLIT = KS::STATIC_TREE ? UR3E_MAIN_SPLIT : 0;
+  int couples = 0; /* a row of this lane has nonzeros in both dof trees */
 #pragma unroll
   for (int h = 0; h < KS::RPL; h++) {
     const int r = lane + 64 * h;
@@ -1375,6 +1410,16 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
 #pragma unroll
       for (int q = 0; q < K_NV; q++)
         if (q < nv) vel += jr[q] * qv[q];
+      if constexpr (SPLIT > 0) {
+        bool a = false, b = false;
+#pragma unroll
+        for (int q = 0; q < K_NV; q++)
+          if (q < nv) {
+            if (q < SPLIT) a = a || jr[q] != 0;
+            else b = b || jr[q] != 0;
+          }
+        couples |= a && b;
+      }
       double imp = k_get_impedance(si, pos, margin);
       double dmax = si[1];
       if (dmax < K_MINIMP) dmax = K_MINIMP;
@@ -1397,6 +1442,10 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
       double R = (1 - imp) * diag / imp;
       s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
     }
+  }
+  if constexpr (SPLIT > 0) {
+    const bool any = __ballot(couples) != 0;
+    if (lane == 0) s.bdiag = !any;
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
