@@ -1885,12 +1885,19 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::OVERLAY); /* compact tier: ur3e_wave_r.h */
+  /* diagnostic builds only (-DUR3E_DOUBLE_STAGE=k): the compact tier runs idempotent stage k twice, so
+     the difference of SQ_INSTS_VALU against the normal build is that stage's instruction count
+     (tools/stage_insts.py); results are unchanged */
+#ifndef UR3E_DOUBLE_STAGE
+#define UR3E_DOUBLE_STAGE -1
+#endif
+#define W_DBL(k, stmt) do { stmt; if (REG && UR3E_DOUBLE_STAGE == (k)) { stmt; } } while (0)
   static_assert(!KS::OVERLAY || REG, "the overlaid layout is only valid for the 64-lane register path");
   WT(23);
   if constexpr (REG) {
     /* the main.xml-specialised kernels only run on models with <= 1 joint per body (host check), so
        the general per-level pass is not compiled into them */
-    if constexpr (KS::STATIC_TREE) r_kinematics(m, pl, s);
+    if constexpr (KS::STATIC_TREE) W_DBL(0, r_kinematics(m, pl, s));
     else if (pl->max_jntnum <= 1) r_kinematics(m, pl, s);
     else w_kinematics<NT>(m, pl, s);
   } else {
@@ -1909,7 +1916,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   WT(3);
   if constexpr (KS::OVERLAY) {
     /* velocity-dependent forces first: their scratch shares bytes with the constraint rows */
-    r_vel_acc(m, pl, s);
+    W_DBL(6, r_vel_acc(m, pl, s));
     /* the epilogue's site velocities (w_obs_v2), while cvel (KB) is alive */
     if (tid < 2) {
       const int site = tid == 0 ? m->id_site_tcp : m->id_site_handle;
@@ -1918,13 +1925,13 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
       for (int k = 0; k < 6; k++) s.site_vel[tid][k] = v[k];
     }
     WT(6);
-    w_rne_passive<NT>(m, pl, s);
+    W_DBL(7, w_rne_passive<NT>(m, pl, s));
     WT(7);
   }
-  w_collision<NT>(m, s);
+  W_DBL(4, w_collision<NT>(m, s));
   WT(4);
   if (KS::BAIL && s.ovf) return;
-  w_make_constraint<NT>(m, pl, s);
+  W_DBL(5, w_make_constraint<NT>(m, pl, s));
   WT(5);
   if (KS::BAIL && s.ovf) return;
   if constexpr (!KS::OVERLAY) {
@@ -1935,7 +1942,8 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
     WT(7);
   }
   if constexpr (REG) {
-    double x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0);
+    double x;
+    W_DBL(8, x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0));
     if (tid < nv) s.qacc_smooth[tid] = x;
     SYNC();
   } else {
@@ -1943,7 +1951,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   WT(8);
   if constexpr (REG)
-    r_solve_newton(m, s);
+    W_DBL(15, r_solve_newton(m, s));
   else
     w_solve_newton<NT>(m, s);
   WT(15);

@@ -719,6 +719,12 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
   return bestA;
 }
 
+/* diagnostic builds only (-DUR3E_DOUBLE_STAGE=20..23): run one Newton component twice (direction,
+   line search, constraint-state evaluation, gradient; each idempotent) for tools/stage_insts.py */
+#ifndef UR3E_DOUBLE_STAGE
+#define UR3E_DOUBLE_STAGE -1
+#endif
+#define RDBL(k, stmt) do { stmt; if (UR3E_DOUBLE_STAGE == (k)) { stmt; } } while (0)
 /* w_solve_newton for the compact tier; leaves s.qacc and s.qfrc_constraint */
 template <class KS>
 WD void r_solve_newton(KModel m, KS& s) {
@@ -739,28 +745,30 @@ WD void r_solve_newton(KModel m, KS& s) {
 #pragma unroll
   for (int h = 0; h < RPL; h++) r_load_rows(m, s, W[h], lane + 64 * h);
   double Ma, gauss, cost;
-  r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
+  RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
   const double cost_ws = cost;
-  r_eval_state(m, s, W, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost);
+  RDBL(22, r_eval_state(m, s, W, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost));
   const double cost_sm = cost;
   if (cost_ws > cost_sm) {
     qacc = lane < nv ? qas : 0.0;
   } else {
-    r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
+    RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
   }
   double qfrc_c, grad;
-  r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad);
+  RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
   WT(9);
-  double search = r_direction(m, s, W, grad);
+  double search;
+  RDBL(20, search = r_direction(m, s, W, grad));
   WT(11);
   for (int iter = 0; iter < m->iterations; iter++) {
-    double alpha = r_line_search(m, s, W, search, Ma, qs, gauss, scale);
+    double alpha;
+    RDBL(21, alpha = r_line_search(m, s, W, search, Ma, qs, gauss, scale));
     WT(13);
     if (alpha == 0) break;
     qacc += alpha * search;
     double oldcost = cost;
-    r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost);
-    r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad);
+    RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
+    RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
     WT(14);
     double gn = 0;
     r_stage(R_SLOT(s, 0), grad);
@@ -774,7 +782,7 @@ WD void r_solve_newton(KModel m, KS& s) {
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
-    search = r_direction(m, s, W, grad);
+    RDBL(20, search = r_direction(m, s, W, grad));
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
