@@ -747,12 +747,26 @@ WD void r_solve_newton(KModel m, KS& s) {
   double Ma, gauss, cost;
   RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
   const double cost_ws = cost;
+  /* the warm start's evaluation is kept: when it wins, the oracle evaluates it again, and that
+     deterministic recomputation (same qacc, same rows) is replaced by restoring what it produces
+     (jar, force, F, state, flag per row; Ma, gauss, cost) */
+  double k_jar[RPL], k_force[RPL], k_F[RPL];
+  int k_st[RPL], k_flag[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; h++) {
+    k_jar[h] = W[h].jar; k_force[h] = W[h].force; k_F[h] = W[h].F; k_st[h] = W[h].st; k_flag[h] = W[h].flag;
+  }
+  const double k_Ma = Ma, k_gauss = gauss;
   RDBL(22, r_eval_state(m, s, W, lane < nv ? qas : 0.0, qs, qas, Ma, gauss, cost));
   const double cost_sm = cost;
   if (cost_ws > cost_sm) {
     qacc = lane < nv ? qas : 0.0;
   } else {
-    RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
+#pragma unroll
+    for (int h = 0; h < RPL; h++) {
+      W[h].jar = k_jar[h]; W[h].force = k_force[h]; W[h].F = k_F[h]; W[h].st = k_st[h]; W[h].flag = k_flag[h];
+    }
+    Ma = k_Ma; gauss = k_gauss; cost = cost_ws;
   }
   double qfrc_c, grad;
   RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
