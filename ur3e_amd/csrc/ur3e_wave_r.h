@@ -466,24 +466,65 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
      (the oracle's left-looking order) */
   /* L[j][j] ends on lane j (h[j]); the solves read it back by readlane instead of keeping a
      per-lane copy of the whole diagonal */
+  if (SPLIT > 0 && bd) {
+    /* block-diagonal: the two blocks factor independently (every update of one block by the other
+       subtracts +0); their columns are interleaved, column t of the first block with column
+       S + t of the second, so the two sqrt / division chains overlap */
+    constexpr int NVS = KS::NV;
 #pragma unroll
-  for (int j = 0; j < K_NV; j++) {
-    if (j < nv) {
+    for (int t = 0; t < SPLIT; t++) {
+      const int j = t, jm = SPLIT + t;
+      const bool mcol = jm < NVS; /* compile-time (t unrolled) */
       double sum = rl(h[j], j);
+      double summ = mcol ? rl(h[jm < K_NV ? jm : 0], jm < K_NV ? jm : 0) : 1.0;
       if (sum < K_MINVAL) sum = K_MINVAL;
-      double ljj = sqrt(sum);
+      if (summ < K_MINVAL) summ = K_MINVAL;
+      const double ljj = sqrt(sum);
+      const double lmm = mcol ? sqrt(summ) : 1.0;
       if (lane > j) h[j] = h[j] / ljj;
       if (lane == j) h[j] = ljj;
-      /* column j to every lane through an LDS slot (broadcast reads, not a readlane per k) */
-      double* col = R_SLOT(s, j & 1);
-      r_stage(col, h[j]);
-      /* block-diagonal: a first-block column updates second-block entries by -(+0 * +0): skipped */
-      const int kend = bd && j < SPLIT ? SPLIT : nv;
+      if (mcol) {
+        double& hm = h[jm < K_NV ? jm : 0];
+        if (lane > jm) hm = hm / lmm;
+        if (lane == jm) hm = lmm;
+      }
+      double* col = R_SLOT(s, t & 1);
+      double* colm = R_SLOT(s, 2);
+      col[lane] = h[j];
+      if (mcol) colm[lane] = h[jm < K_NV ? jm : 0];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = j + 1; k < K_NV; k++) {
-        if (k < kend) {
-          const double lkj = col[k];
-          if (lane >= k) h[k] -= h[j] * lkj;
+      for (int k = j + 1; k < SPLIT; k++) {
+        const double lkj = col[k];
+        if (lane >= k) h[k] -= h[j] * lkj;
+      }
+      if (mcol) {
+#pragma unroll
+        for (int k = jm + 1; k < NVS; k++) {
+          const double lkm = colm[k];
+          if (lane >= k) h[k] -= h[jm < K_NV ? jm : 0] * lkm;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K_NV; j++) {
+      if (j < nv) {
+        double sum = rl(h[j], j);
+        if (sum < K_MINVAL) sum = K_MINVAL;
+        double ljj = sqrt(sum);
+        if (lane > j) h[j] = h[j] / ljj;
+        if (lane == j) h[j] = ljj;
+        /* column j to every lane through an LDS slot (broadcast reads, not a readlane per k) */
+        double* col = R_SLOT(s, j & 1);
+        r_stage(col, h[j]);
+#pragma unroll
+        for (int k = j + 1; k < K_NV; k++) {
+          if (k < nv) {
+            const double lkj = col[k];
+            if (lane >= k) h[k] -= h[j] * lkj;
+          }
         }
       }
     }
