@@ -187,11 +187,13 @@ template <class KS>
 WD double r_row_dot(const KS& s, int nv, int nefc, const double x[K_NV], int row) {
   const bool act = row < nefc;
   const int r = act ? row : 0;
+  /* an inactive row's terms are 0.0 * x[k] = +-0, whose ordered sum from +0 is +0: it returns 0.0
+     after the sum instead of selecting 0.0 per element (same value for finite x) */
   double v = 0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++)
-    if (k < nv) v += (act ? s.efc_J[r][k] : 0.0) * x[k];
-  return v;
+    if (k < nv) v += s.efc_J[r][k] * x[k];
+  return act ? v : 0.0;
 }
 
 /* Ordered sums and vector broadcasts inside Newton go through a 64*RPL-double LDS slot per operand
@@ -674,14 +676,15 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
     b1[lane + 64 * h] = dFm[h];
   }
   r_stage_rows(b2, d2Fm);
+  /* the three ordered sums run on lanes 0, 1, 2 (lane k reads slot k; the others repeat lane 0's):
+     one LDS read and one add per row instead of three, same operands in the same order */
+  const int sel = lane == 1 ? 1 : (lane == 2 ? 2 : 0);
+  const double* bs = R_SLOT(s, sel);
+  double acc = sel == 0 ? aF : (sel == 1 ? adF : ad2F);
 #pragma unroll 4
-  for (int i = 0; i < nefc; i++) {
-    aF += b0[i];
-    adF += b1[i];
-    ad2F += b2[i];
-  }
+  for (int i = 0; i < nefc; i++) acc += bs[i];
   r_slot_done();
-  lsF = aF; lsdF = adF; lsd2F = ad2F;
+  lsF = rl(acc, 0); lsdF = rl(acc, 1); lsd2F = rl(acc, 2);
 }
 
 /* w_line_search: returns alpha (uniform); Jv on the row lanes */
@@ -714,17 +717,18 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
   for (int h = 0; h < RPL; h++) W[h].Jv = r_row_dot(s, nv, nefc, sv, lane + 64 * h);
   if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
-  double g1 = 0, g2 = 0;
   R_SLOT(s, 1)[lane] = t1;
   r_stage(R_SLOT(s, 2), t2);
+  /* g1 on lane 1 (and the others), g2 on lane 2, as in r_ls_eval */
+  double gacc = 0;
+  {
+    const double* gs = R_SLOT(s, lane == 2 ? 2 : 1);
 #pragma unroll
-  for (int k = 0; k < K_NV; k++) {
-    if (k < nv) {
-      g1 += R_SLOT(s, 1)[k];
-      g2 += R_SLOT(s, 2)[k];
-    }
+    for (int k = 0; k < K_NV; k++)
+      if (k < nv) gacc += gs[k];
   }
   r_slot_done();
+  const double g1 = rl(gacc, 1), g2 = rl(gacc, 2);
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
   RLs lc[RPL];
