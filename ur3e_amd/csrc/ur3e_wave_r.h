@@ -254,22 +254,28 @@ WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs
   for (int h = 0; h < RPL; h++) W[h].jar = r_row_dot(s, nv, nefc, qv, lane + 64 * h) - W[h].aref;
   r_constraint_update(W);
   double term = (Ma - qs) * (qacc - qas);
-  double a0 = 0, a1 = 0;
   /* skipped rows contribute -0.0: x + (-0.0) == x exactly for every x (incl. -0, inf, NaN), so
      the ordered sum needs neither a branch nor a select per row */
-  double Fm0[RPL];
+  double Fm0[RPL], Tm0[RPL];
 #pragma unroll
-  for (int h = 0; h < RPL; h++) Fm0[h] = W[h].flag ? W[h].F : -0.0;
+  for (int h = 0; h < RPL; h++) {
+    Fm0[h] = W[h].flag ? W[h].F : -0.0;
+    Tm0[h] = h == 0 && lane < nv ? term : -0.0;
+  }
   double* st = R_SLOT(s, 1);
   double* sf = R_SLOT(s, 2);
-  st[lane] = term;
-  r_stage_rows(sf, Fm0);
 #pragma unroll
-  for (int i = 0; i < K_NV; i++)
-    if (i < nv) a0 += st[i];
+  for (int h = 0; h < RPL; h++) st[lane + 64 * h] = Tm0[h];
+  r_stage_rows(sf, Fm0);
+  /* the gauss sum (dofs) on lane 0 and the constraint sum (rows) on lane 1, both over
+     max(nv, nefc) entries: the tails are -0.0, so each equals its own ordered sum */
+  const int nsum = nv > nefc ? nv : nefc;
+  const double* ss = lane == 1 ? sf : st;
+  double acc = 0;
 #pragma unroll 4
-  for (int i = 0; i < nefc; i++) a1 += sf[i];
+  for (int i = 0; i < nsum; i++) acc += ss[i];
   r_slot_done();
+  const double a0 = rl(acc, 0), a1 = rl(acc, 1);
   gauss = 0.5 * a0;
   cost = gauss + a1;
 }
@@ -699,11 +705,6 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
 #pragma unroll
   for (int k = 0; k < K_NV; k++) sv[k] = R_SLOT(s, 0)[k];
   r_slot_done();
-  double sn = 0;
-#pragma unroll
-  for (int k = 0; k < K_NV; k++)
-    if (k < nv) sn += sv[k] * sv[k];
-  double snorm = sqrt(sn);
   double Mv;
   {
     double v = 0;
@@ -715,19 +716,22 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
   }
 #pragma unroll
   for (int h = 0; h < RPL; h++) W[h].Jv = r_row_dot(s, nv, nefc, sv, lane + 64 * h);
-  if (snorm < K_MINVAL) return 0;
   double t1 = search * (Ma - qs), t2 = search * Mv;
+  /* three ordered sums over the dofs on lanes 0, 1, 2 as in r_ls_eval: |search|^2 from the squares
+     each lane stages (search_k * search_k, the product every lane formed before), g1, g2 */
+  R_SLOT(s, 0)[lane] = search * search;
   R_SLOT(s, 1)[lane] = t1;
   r_stage(R_SLOT(s, 2), t2);
-  /* g1 on lane 1 (and the others), g2 on lane 2, as in r_ls_eval */
   double gacc = 0;
   {
-    const double* gs = R_SLOT(s, lane == 2 ? 2 : 1);
+    const double* gs = R_SLOT(s, lane == 1 ? 1 : (lane == 2 ? 2 : 0));
 #pragma unroll
     for (int k = 0; k < K_NV; k++)
       if (k < nv) gacc += gs[k];
   }
   r_slot_done();
+  const double snorm = sqrt(rl(gacc, 0));
+  if (snorm < K_MINVAL) return 0;
   const double g1 = rl(gacc, 1), g2 = rl(gacc, 2);
   double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
   double f0, d0, h0;
@@ -829,14 +833,12 @@ WD void r_solve_newton(KModel m, KS& s) {
     RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
     RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
     WT(14);
+    /* lane i stages grad_i * grad_i (the product every lane formed before), then one ordered sum */
     double gn = 0;
-    r_stage(R_SLOT(s, 0), grad);
+    r_stage(R_SLOT(s, 0), grad * grad);
 #pragma unroll
     for (int i = 0; i < K_NV; i++)
-      if (i < nv) {
-        const double gi = R_SLOT(s, 0)[i];
-        gn += gi * gi;
-      }
+      if (i < nv) gn += R_SLOT(s, 0)[i];
     r_slot_done();
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
