@@ -483,18 +483,22 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
     for (int t = 0; t < SPLIT; t++) {
       const int j = t, jm = SPLIT + t;
       const bool mcol = jm < NVS; /* compile-time (t unrolled) */
+      /* one square root and one division per step serve both columns: lanes [0, S) take the first
+         block's pivot and entries, lanes [S, ...) the second's (the first block's column on those
+         lanes is the cross block's +0, left as it is: +0 / pivot would give +0 again) */
+      const bool lb = lane >= SPLIT;
       double sum = rl(h[j], j);
       double summ = mcol ? rl(h[jm < K_NV ? jm : 0], jm < K_NV ? jm : 0) : 1.0;
-      if (sum < K_MINVAL) sum = K_MINVAL;
-      if (summ < K_MINVAL) summ = K_MINVAL;
-      const double ljj = sqrt(sum);
-      const double lmm = mcol ? sqrt(summ) : 1.0;
-      if (lane > j) h[j] = h[j] / ljj;
-      if (lane == j) h[j] = ljj;
+      double piv = lb ? summ : sum;
+      if (piv < K_MINVAL) piv = K_MINVAL;
+      const double lp = sqrt(piv); /* lane < S: L[j][j]; lane >= S: L[jm][jm] (1 when !mcol) */
+      double& hm = h[jm < K_NV ? jm : 0];
+      const double q = (lb ? hm : h[j]) / lp;
+      if (!lb && lane > j) h[j] = q;
+      if (lane == j) h[j] = lp;
       if (mcol) {
-        double& hm = h[jm < K_NV ? jm : 0];
-        if (lane > jm) hm = hm / lmm;
-        if (lane == jm) hm = lmm;
+        if (lane > jm) hm = q;
+        if (lane == jm) hm = lp;
       }
       double* col = R_SLOT(s, t & 1);
       double* colm = R_SLOT(s, 2);
