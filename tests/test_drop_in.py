@@ -75,10 +75,22 @@ SCRIPT = textwrap.dedent("""
         ends += int(dones.sum())
     out.update(obs=list(obs.shape), rew=list(rew.shape), ends=ends)
     if os.environ.get("DROPIN_GPU"):
-        vn = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10)
+        # train_rl.py:20 names the statistics file; :46-57 resume or start; :90 saves
+        save_dir = "policies/rl_policies"
+        os.makedirs(save_dir, exist_ok=True)
+        vecnormalize_fpath = f"{save_dir}/rl_vecnormalize_l.pkl"
+        resume_training = bool(os.environ.get("DROPIN_RESUME"))
+        if resume_training and os.path.exists(vecnormalize_fpath):
+            vn = VecNormalize.load(vecnormalize_fpath, venv)
+        else:
+            vn = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10)
+        out["rms_loaded"] = [float(vn.obs_rms.count)] + [float(x) for x in vn.obs_rms.mean]
         o = vn.reset()
         o, r, d, i = vn.step(np.tile(venv.action_space.low, (n_envs, 1)))
         out.update(vecnormalize=type(vn).__module__, vn_obs_dtype=str(o.dtype))
+        vn.save(vecnormalize_fpath)
+        out["saved_files"] = sorted(os.listdir(save_dir))
+        out["rms_saved"] = [float(vn.obs_rms.count)] + [float(x) for x in vn.obs_rms.mean]
     out["other_id"] = list(make_vec_env("CartPole-v1", n_envs=2))
     print("RESULT " + json.dumps(out))
 """)
@@ -95,7 +107,7 @@ BOOT_CPU = textwrap.dedent("""
 """)
 
 
-def _run(tmp_path, gpu: bool):
+def _run(tmp_path, gpu: bool, resume: bool = False):
     for rel, txt in SB3_STUBS.items():
         p = tmp_path / rel
         p.parent.mkdir(parents=True, exist_ok=True)
@@ -106,6 +118,8 @@ def _run(tmp_path, gpu: bool):
     env["PYTHONPATH"] = os.pathsep.join([str(tmp_path), REPO])
     if gpu:
         env["DROPIN_GPU"] = "1"
+        if resume:
+            env["DROPIN_RESUME"] = "1"
         cmd = [sys.executable, str(script)]
     else:
         boot = tmp_path / "boot.py"
@@ -140,6 +154,34 @@ def test_train_rl_script_drops_in_gpu(tmp_path):
     out = _run(tmp_path, gpu=True)
     _check(out)
     assert out["vecnormalize"] == "ur3e_amd.envs.vec_normalize" and out["vn_obs_dtype"] == "float32"
+    # train_rl.py:90 saves to exactly the .pkl name, and the resume branch (:46-49) loads it back
+    assert out["saved_files"] == ["rl_vecnormalize_l.pkl"]
+    out2 = _run(tmp_path, gpu=True, resume=True)
+    _check(out2)
+    assert out2["rms_loaded"] == out["rms_saved"]
+    assert out2["rms_saved"][0] > out["rms_saved"][0]  # the resumed run kept counting
+
+
+def test_vecnormalize_stats_file_exact_path(tmp_path):
+    """save() writes exactly the path it is given (np.savez would append .npz to '...pkl'); load reads it,
+    a file left at path + '.npz' by an older build is still found, anything else is refused."""
+    import numpy as np
+    from ur3e_amd.envs.vec_normalize import STATS_KEYS, read_stats, write_stats
+    arrays = {k: np.arange(3, dtype=np.float64) + i for i, k in enumerate(STATS_KEYS)}
+    p = tmp_path / "rl_vecnormalize_l.pkl"
+    write_stats(str(p), **arrays)
+    assert sorted(os.listdir(tmp_path)) == ["rl_vecnormalize_l.pkl"]
+    back = read_stats(str(p))
+    assert all(np.array_equal(back[k], arrays[k]) for k in STATS_KEYS)
+    old = tmp_path / "old.pkl"
+    np.savez(str(old), **arrays)  # the old save(): lands at old.pkl.npz
+    assert np.array_equal(read_stats(str(old))["cfg"], arrays["cfg"])
+    bad = tmp_path / "sb3.pkl"
+    bad.write_bytes(b"\x80\x04not a zip")
+    with pytest.raises(ValueError):
+        read_stats(str(bad))
+    with pytest.raises(FileNotFoundError):
+        read_stats(str(tmp_path / "missing.pkl"))
 
 
 def test_install_drop_in_namespace():

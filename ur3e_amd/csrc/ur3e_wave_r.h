@@ -363,6 +363,10 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
      element slots per lane instead of four) and the factorisation skips the cross updates; the
      triangular solves stay dense. */
   constexpr int SPLIT = KS::STATIC_TREE ? UR3E_MAIN_SPLIT : 0;
+  /* the interleaved block Cholesky below runs t < SPLIT and factors the second block's column
+     SPLIT + t in step t: it needs the trailing tree to be no larger than the leading one */
+  static_assert(UR3E_MAIN_SPLIT == 0 || UR3E_MAIN_NV - UR3E_MAIN_SPLIT <= UR3E_MAIN_SPLIT,
+                "block Cholesky: trailing dof tree larger than the leading one");
   const bool bd = SPLIT > 0 && s.bdiag;
 #ifdef UR3E_STAGE_TIMING
   if (lane == 0 && bd) s.tcnt[28] += 1; /* diagnostic: block-diagonal Newton directions */

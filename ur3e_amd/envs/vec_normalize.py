@@ -15,8 +15,9 @@ statistics kernel over the whole global batch: the statistics, the per-env disco
 normalised outputs are then identical on every rank and identical to a single-process VecNormalize over
 all envs; each rank keeps its own rows.
 
-Persistence: `save(path)` / `VecNormalize.load(path, venv)` write the statistics and settings to an
-.npz (SB3 pickles the wrapper object; its fields are the same).
+Persistence: `save(path)` / `VecNormalize.load(path, venv)` write the statistics and settings as an
+.npz archive at exactly `path`, whatever its suffix (train_rl.py:20,90 save to `rl_vecnormalize_*.pkl`
+and :49 / evaluate_rl.py:30 load that same name; SB3 pickles the wrapper object, its fields are the same).
 """
 from __future__ import annotations
 
@@ -25,6 +26,39 @@ import ctypes
 import numpy as np
 
 from .. import runtime as rt
+
+
+STATS_KEYS = ("obs_mean", "obs_var", "obs_count", "ret_mean", "ret_var", "ret_count", "cfg")
+
+
+def write_stats(path, **arrays):
+    """np.savez into exactly `path` (whatever its suffix)."""
+    missing = set(STATS_KEYS) - set(arrays)
+    if missing:
+        raise ValueError(f"VecNormalize statistics lack {sorted(missing)}")
+    with open(path, "wb") as f:
+        np.savez(f, **arrays)
+
+
+def read_stats(path) -> dict:
+    """The arrays write_stats() stored at `path`.  A file saved by an older build of this package at
+    `path + '.npz'` (np.savez's suffix) is read too.  Anything that is not such an .npz raises."""
+    import os
+    import zipfile
+    p = str(path)
+    if not os.path.exists(p) and os.path.exists(p + ".npz"):
+        p = p + ".npz"
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"no VecNormalize statistics at {path!r}")
+    if not zipfile.is_zipfile(p):
+        raise ValueError(f"{p!r} is not a VecNormalize .npz written by ur3e_amd (SB3 pickles are not "
+                         "loaded: re-save the statistics with VecNormalize.save from this package)")
+    with np.load(p) as z:  # allow_pickle=False
+        out = {k: z[k] for k in z.files}
+    missing = set(STATS_KEYS) - set(out)
+    if missing:
+        raise ValueError(f"{p!r} lacks VecNormalize fields {sorted(missing)}")
+    return out
 
 
 class StatsC(ctypes.Structure):
@@ -240,24 +274,23 @@ class VecNormalize:
         self.venv.close()
 
     def save(self, path):
-        np.savez(path, obs_mean=self.obs_rms.mean, obs_var=self.obs_rms.var, obs_count=self.obs_rms.count,
-                 ret_mean=self.ret_rms.mean, ret_var=self.ret_rms.var, ret_count=self.ret_rms.count,
-                 cfg=np.array([self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward,
-                               self.gamma, self.epsilon], dtype=np.float64))
+        """Write the statistics and settings to exactly `path` (train_rl.py:90 names it `...pkl`;
+        np.savez on a str would append `.npz`, so it gets an open file instead)."""
+        write_stats(path, obs_mean=self.obs_rms.mean, obs_var=self.obs_rms.var, obs_count=self.obs_rms.count,
+                    ret_mean=self.ret_rms.mean, ret_var=self.ret_rms.var, ret_count=self.ret_rms.count,
+                    cfg=np.array([self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward,
+                                  self.gamma, self.epsilon], dtype=np.float64))
 
     @classmethod
-    def load(cls, path, venv):
-        """Load statistics written by save() (.npz).  SB3's VecNormalize.load reads a pickle of the whole
-        wrapper (train_rl.py's resume branch); pickles are never loaded here (they execute code), so an
-        SB3 file is refused with a clear message instead of failing inside np.load."""
-        import zipfile
-        if not zipfile.is_zipfile(path):
-            raise ValueError(f"{path!r} is not a VecNormalize .npz written by ur3e_amd (SB3 pickles are not "
-                             "loaded: re-save the statistics with VecNormalize.save from this package)")
-        z = np.load(path)  # allow_pickle=False
+    def load(cls, path, venv, group=None):
+        """Load statistics written by save() (train_rl.py:49 / evaluate_rl.py:30 pass the path save() got).
+        SB3's VecNormalize.load reads a pickle of the whole wrapper; pickles are never loaded here (they
+        execute code), so an SB3 file is refused with a clear message instead of failing inside np.load.
+        `group`: the process group of a multi-rank run, as in __init__ (the statistics stay global)."""
+        z = read_stats(path)
         c = z["cfg"]
         self = cls(venv, training=bool(c[0]), norm_obs=bool(c[1]), norm_reward=bool(c[2]), clip_obs=float(c[3]),
-                   clip_reward=float(c[4]), gamma=float(c[5]), epsilon=float(c[6]))
+                   clip_reward=float(c[4]), gamma=float(c[5]), epsilon=float(c[6]), group=group)
         t = self.torch
         self._obs_mean.copy_(t.from_numpy(z["obs_mean"]))
         self._obs_var.copy_(t.from_numpy(z["obs_var"]))
