@@ -419,7 +419,8 @@ def main():
             "data": "synthetic (uniform random actions in the ur3e-v2 action Box, generated into HBM before the timed region; stochastic 'high' mug resets; timed window starts after --pre-steps untimed env-steps, mid-episode)",
             "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
-                       "kernel_layout": {0: "two-tier: compact 64-lane wavefront per env (20 KB lifetime-overlaid LDS working set, 256 VGPRs: 8 envs/CU, 2 per SIMD)"
+                       "kernel_layout": {0: f"two-tier: compact 64-lane wavefront per env ({batch_kinfo.get('lds_bytes')} B lifetime-overlaid LDS working set,"
+                                               f" {batch_kinfo.get('regs')} VGPRs: {batch_kinfo.get('envs_per_cu')} envs/CU)"
                                             " + full-capacity fallback; above the resident slot count the compact tier runs as a"
                                             " substep work queue", -128: "full-capacity, 128 lanes per env",
                                             -64: "full-capacity, 64 lanes per env"}.get(

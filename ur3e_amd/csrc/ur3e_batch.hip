@@ -1215,6 +1215,13 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
 #ifdef UR3E_WAVE_TRACE
 #define UR3E_WAVE_TRACE_MAX 16384
 __device__ unsigned long long ur3e_wave_trace[UR3E_WAVE_TRACE_MAX][4];
+/* which lanes store the queue kernel's unit stamps: every lane (same word, same value; default) or
+   lane 0 alone (-DUR3E_TRACE_LANE0) */
+#ifdef UR3E_TRACE_LANE0
+#define W_TRACE_LANES (threadIdx.x == 0)
+#else
+#define W_TRACE_LANES true
+#endif
 #endif
 
 /* XCD-aware env order: workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8), so workgroup
@@ -1336,7 +1343,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     const int e0 = q * nper + (u - sub * nper);
     if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
-    if (sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime(); /* every lane, same word: no exec-masked region */
+    if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (sub > 0) {
       if (tid == 0) {
@@ -1365,7 +1372,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
     }
 #ifdef UR3E_WAVE_TRACE
-    if (sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime(); /* every lane, same word: no exec-masked region */
+    if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, sub, sub + 1, mid);
     const int r = __builtin_amdgcn_readfirstlane(r0);
@@ -1392,7 +1399,7 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
     SYNC();
 #ifdef UR3E_WAVE_TRACE
     /* per unit (sub * n + e): pulled, flag acquired, finished (s_memrealtime), workgroup | XCC << 32 */
-    if (sub * n + e < UR3E_WAVE_TRACE_MAX) {
+    if (W_TRACE_LANES && sub * n + e < UR3E_WAVE_TRACE_MAX) {
       unsigned long long* tr = ur3e_wave_trace[sub * n + e];
       tr[2] = __builtin_amdgcn_s_memrealtime();
       tr[3] = (unsigned long long)blockIdx.x |
