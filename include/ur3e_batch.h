@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 5
+#define UR3E_ABI_VERSION 6
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -175,6 +175,17 @@ int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
    rows; it runs on an
    internal stream concurrently with the compact tier) */
 int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
+
+/* substep work queue (schedule 1), since create (synchronises): stats[0] units that gave up waiting
+   for their producer (spin limit; the env-step then ran in the fallback tiers), stats[1] static
+   first units that were claimed and run by their consumer because their own workgroup was not
+   running yet.  Neither changes results. */
+int ur3e_batch_queue_stats(ur3e_batch_t* b, unsigned long long* stats);
+
+/* diagnostics of the substep work queue (results never change): spin_limit = flag polls before a
+   waiting unit gives up (0 = the built-in bound, 2^26); leave_static_units = 1: workgroups skip their
+   static first units, so every one of them is claimed and run by its consumer */
+int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int leave_static_units);
 
 /* the step kernel this handle launches: 0 compact tier, one workgroup per env-step; 1 compact tier
    as a substep work queue; 2 full-capacity tier only; 3 one env per lane (v1) */

@@ -130,6 +130,11 @@ class OracleBatch:
             self.L.ur3o_env_sensordata(ctypes.byref(self.m), ptr, _p(out[i]))
         return out[:, :nsd]
 
+    def get_ctrl(self):
+        """[n, nu] d.ctrl applied by every env's last step"""
+        nu = self.m.nu
+        return np.stack([self.diag(i)["ctrl"][:nu] for i in range(self.n)])
+
     def diag(self, i):
         ncon, nefc, nit = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         touch = np.zeros(4)

@@ -101,7 +101,7 @@ BOOT_CPU = textwrap.dedent("""
     sys.path.insert(0, {repo!r})
     import ur3e_amd.envs.vec_env as ve
     from tests.helpers import OracleStepper
-    ve._default_stepper = lambda env_id, n, device, seed, off, epb, T: OracleStepper(
+    ve._default_stepper = lambda env_id, n, device, seed, off, epb, T, cfg_yaml=None: OracleStepper(
         n, seed=seed, env_id_offset=off, max_episode_steps=3 if T is None else T, env_id=env_id)
     runpy.run_path({script!r}, run_name="__main__")
 """)

@@ -1,0 +1,48 @@
+"""GPU: an edited config_l_mug.yml gain reaches the kernel's controller through the drop-in facade, and
+the GPU and the oracle apply it identically (ur3e_env2.py:66-68 reads the YAML at construction)."""
+import numpy as np
+import pytest
+import yaml
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([0.04799994, -0.11650084, 0.0, 0.0])
+HI = np.array([0.54799994, 0.38349916, 0.5, 1.0])
+
+
+def test_edited_yaml_gain_changes_ctrl_identically(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import pyoracle as po
+    from ur3e_amd import gains
+    from ur3e_amd.envs.vec_env import UR3eVecEnv
+    with open(gains.config_path("config_l_mug.yml")) as f:
+        d = yaml.safe_load(f)
+    d["pos"]["kp"] = [180.0, 260.0, 90.0]
+    d["rot"]["kd"] = [3.0, 1.5, 2.5]
+    p = tmp_path / "config_l_mug.yml"
+    with open(p, "w") as f:
+        yaml.safe_dump(d, f, sort_keys=False)
+    n, steps = 64, 20
+    ve = UR3eVecEnv(num_envs=n, seed=5, config_yaml_path=str(p))
+    vd = UR3eVecEnv(num_envs=n, seed=5)
+    assert ve.stepper.cfg.task_gains[0] == 180.0 and vd.stepper.cfg.task_gains[0] == 220.0
+    ob = po.OracleBatch(ve.stepper.model_c, po.config_from(ve.stepper.cfg), n)
+    ve.reset()
+    vd.reset()
+    rng = np.random.default_rng(2)
+    differs = False
+    for t in range(steps):
+        a = rng.uniform(LO, HI, size=(n, 4))
+        o = ob.step(a)
+        obs, rew, done, infos = ve.step(a)
+        vd.step(a)
+        ctrl_e = ve.stepper.get_ctrl().cpu().numpy()
+        ctrl_d = vd.stepper.get_ctrl().cpu().numpy()
+        assert np.array_equal(obs, o[0]) and np.array_equal(rew, o[1]), f"step {t}"
+        assert np.array_equal(ctrl_e, ob.get_ctrl()), f"ctrl step {t}"
+        differs |= not np.array_equal(ctrl_e, ctrl_d)
+    assert differs, "the edited gains never changed ctrl"
+    ve.close()
+    vd.close()

@@ -8,12 +8,10 @@ import ctypes, json, os, subprocess, sys
 import numpy as np
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, REPO)
-LIB = os.environ.get("UR3E_TRACE_LIB") or os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_trace.so")
+from ur3e_amd import _build
+LIB = os.environ.get("UR3E_TRACE_LIB") or _build.TRACE_LIB
 if not os.path.exists(LIB):
-    from ur3e_amd import _build
-    subprocess.run([_build.HIPCC] + _build.FLAGS + ["-DUR3E_WAVE_TRACE", "-o", LIB,
-                    os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip"),
-                    os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_vecnorm.hip")], check=True)
+    _build.build(trace=True)
 
 if __name__ == "__main__":
     product = len(sys.argv) > 4 and sys.argv[4] == "product"  # the product library: steps only, no trace

@@ -59,8 +59,9 @@ class DemoCollector:
 
     def __init__(self, n_demos: int, action_mode: str = "indirect", reset_mode: str = "stochastic",
                  noise_mag: str = "low", down_sample: int = 1, seed: int = 0, device: int = 0, noise=None,
-                 envs_per_block: int = 0):
+                 envs_per_block: int = 0, config_yaml_path: str | None = None):
         import torch
+        from .. import gains
         from .. import runtime as rt
         if action_mode not in ("indirect", "direct"):
             raise ValueError(f"action_mode must be 'indirect' or 'direct', got {action_mode!r}")
@@ -73,7 +74,8 @@ class DemoCollector:
         rn = NOISE[noise_mag] if reset_mode == "stochastic" else 0
         cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
                              reset_noise=rn, reset_key=md["id_key_down"], model=md, seed=seed,
-                             envs_per_block=envs_per_block)
+                             envs_per_block=envs_per_block,
+                             task_gains=gains.task_gains(config_yaml_path))  # collect_demos.py:89-94
         self.batch = rt.Batch(mc, cfg, n_demos, device=device)
         dev = self.batch.device
         n = n_demos

@@ -47,17 +47,20 @@ class MoveLMug:
     """N scripted pick-and-place episodes stepping in lock-step."""
 
     def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
-                 envs_per_block: int = 0, sensors: bool = False):
+                 envs_per_block: int = 0, sensors: bool = False, config_yaml_path: str | None = None):
         """sensors=True also records mjData.sensordata every row (actuator_frc[t] = get_jnt_torques(d),
         move_l_mug.py:80), at the cost of the full-capacity kernel (see ur3e_config_t.sensors)."""
         import torch
+        from .. import gains
         from .. import runtime as rt
         self.torch = torch
         md, mc = rt.load_model("main")
         self.md = md
+        # controller/move_l_mug.py:20-26: gains from config_l_mug.yml
         cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
                              reset_noise=NOISE[reset_mode], reset_key=md["id_key_down"], model=md, seed=seed,
-                             envs_per_block=envs_per_block, sensors=sensors)
+                             envs_per_block=envs_per_block, sensors=sensors,
+                             task_gains=gains.task_gains(config_yaml_path))
         self.batch = rt.Batch(mc, cfg, n_envs, device=device)   # reset_with_mug (keyframe + forward)
         obs = self.batch.obs
         start = task_space_state(self.batch)

@@ -403,6 +403,7 @@ struct KState {
 /* host-side routing decision (ur3e_batch_step): run-ahead bound and how long routing stays on after
    the host last saw a routed env */
 #define W_AHEAD 16
+#define W_NTOTAL 5 /* device counters of ur3e_batch::d_ovf_total */
 #define W_ROUTE_HOLD 64
 /* grasp-tier workgroups for the compact tier's bails while routing is off (bails are rare then) */
 #define W_GRASP_IDLE_GRID 128
@@ -417,6 +418,8 @@ struct KConfig {
   int np_lanes; /* survivor lanes per compact narrowphase chunk (1..W_NP_LANES) */
   int obs_sites; /* model has tcp / handle_site / ghost: the scripted tasks also emit the 24-d obs */
   int sensors;   /* compute and store mjData.sensordata every forward (full-capacity kernels) */
+  unsigned int spin_limit; /* substep queue: flag polls before a waiting unit gives up (diagnostic knob) */
+  int leave_static;        /* substep queue diagnostic: owners skip their static units (consumers claim them) */
   KGains gains;
 };
 
@@ -1282,12 +1285,22 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
    balanced at substep granularity, so the launch ends about half an env-step after the average
    instead of a whole slow env-step after it (a 4,096-env launch runs 2,048 envs at a time).
    Results are identical to w_env_step: every env runs the same substeps in the same order.
-   qctl = {next unit, workgroups done, epoch}: the last workgroup to finish re-zeroes the counters
-   and advances the epoch, so the flags of this launch (epoch << 4 | substeps done, or
-   epoch << 4 | 15 once the env bailed to the full-capacity tier) never match a later launch's.
-   A producer unit was pulled before its consumer by a running workgroup and always releases its
-   flag (done or bailed), so every wait ends; the spin is bounded anyway, and a consumer that gives
-   up claims the env for the full-capacity tier instead (atomic exchange: exactly one appender). */
+   qctl = {next unit per queue, workgroups done, epoch}: the last workgroup to finish re-zeroes the
+   counters and advances the epoch, so the flags of this launch (epoch << 4 | substeps done,
+   epoch << 4 | W_FLAG_CLAIMED while substep 0 runs, epoch << 4 | W_FLAG_BAILED once the env went to
+   the fallback tiers) never match a later launch's.
+   Forward progress.  Each workgroup's first unit is static (its rank in its queue, substep 0 only;
+   the counters start past them), so a static unit may belong to a workgroup that is not resident
+   yet -- e.g. while another queue launch or the grasp pre-pass holds the slots.  Static units are
+   therefore claimed: the owner runs one only after moving its flag from an older epoch to CLAIMED
+   (compare-and-swap), and a substep-1 unit that finds its producer static and unclaimed claims it
+   the same way and runs substeps 0 and 1 itself.  Every other producer was pulled from a counter
+   by a running workgroup, before its consumer, and does not wait on anything that is not also
+   running; so every wait ends while only resident workgroups make progress.  The spin stays
+   bounded (KConfig.spin_limit polls): a unit that gives up claims the env for the fallback tiers
+   (atomic exchange: exactly one appender), which recompute the env-step from the committed state,
+   and counts the give-up (queue_stats[0]). */
+#define W_FLAG_CLAIMED 14
 #define W_FLAG_BAILED 15
 #define W_SPIN_LIMIT (1u << 26)
 #define W_NQUEUE 8 /* one unit queue per XCD (workgroup b serves queue b % 8: speed only) */
@@ -1303,10 +1316,11 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
                                                                   unsigned char* __restrict__ trunc_out,
                                                                   double* __restrict__ tobs_out, int* __restrict__ ovf_list,
                                                                   int* ovf_ctl, int* qctl, int* flags,
-                                                                  double* __restrict__ mid) {
+                                                                  double* __restrict__ mid,
+                                                                  unsigned long long* qstats) {
   __shared__ KS s;
   __shared__ WOut o;
-  __shared__ int s_u, s_epoch, s_flag;
+  __shared__ int s_u, s_epoch, s_flag, s_from;
   const int tid = threadIdx.x;
   const int n = st.n, fs = c.frame_skip;
   /* env partition: XCD-sized queues when n splits evenly, else one queue */
@@ -1314,6 +1328,9 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
   const int q = (int)blockIdx.x % nq;
   const int nper = n / nq;
   const int total = nper * fs;
+  /* static first units per queue: substep-0 units only */
+  const int nstat = min((int)gridDim.x / nq, nper);
+  const unsigned int spin_limit = c.spin_limit ? c.spin_limit : W_SPIN_LIMIT;
   if (tid == 0) s_epoch = __hip_atomic_load(qctl + W_NQUEUE + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   SYNC();
   /* wave-uniform values read from LDS pass through readfirstlane so they live in SGPRs: kept in
@@ -1327,9 +1344,10 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
   /* the first unit of every workgroup is static (its rank in its queue; the counters start at the
      number of workgroups per queue): 2,048 workgroups contending for eight counters at once cost
      ~10 us of the launch */
-  int first = 1;
+  int first = (int)blockIdx.x / nq < nstat;
   for (;;) {
     int u;
+    const int is_static = first;
     if (first) {
       u = (int)blockIdx.x / nq;
       first = 0;
@@ -1345,20 +1363,53 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
 #ifdef UR3E_WAVE_TRACE
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (sub > 0) {
+    int from = sub; /* first substep this unit runs */
+    if (is_static) {
+      /* claim the static unit; a consumer may have claimed it (and run it) already */
+      if (tid == 0) {
+        const int f = w_flag_poll(flags + e0);
+        int ok = 0;
+        if ((f >> 4) != E && !c.leave_static) {
+          int expect = f;
+          ok = __hip_atomic_compare_exchange_strong(flags + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_flag = ok;
+      }
+      SYNC();
+      if (!__builtin_amdgcn_readfirstlane(s_flag)) continue;
+    } else if (sub > 0) {
       if (tid == 0) {
         const int want = (E << 4) | sub;
         int f = w_flag_poll(flags + e0);
+        int fr = sub;
+        /* producer is a static substep-0 unit not claimed yet: claim it and run both substeps */
+        if (sub == 1 && u - nper < nstat && (f >> 4) != E) {
+          int expect = f;
+          if (__hip_atomic_compare_exchange_strong(flags + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            fr = 0;
+            f = want;
+            atomicAdd(qstats + 1, 1ull);
+          } else {
+            f = expect; /* claimed (or finished) by its owner meanwhile: wait for it below */
+          }
+        }
         unsigned int spins = 0;
         while (f != want && f != bailed) {
-          if (++spins > W_SPIN_LIMIT) {
+          if (++spins > spin_limit) {
             const int old = atomicExch(flags + e0, bailed);
             if (old == want) {
               f = want; /* released while we gave up: keep going (and keep the flag final) */
               atomicExch(flags + e0, want);
             } else {
               f = bailed;
-              if (old != bailed) ovf_list[min(atomicAdd(ovf_ctl, 1), n - 1)] = e0;
+              if (old != bailed) {
+                /* the env goes to the fallback tiers, which recompute its env-step (one appender) */
+                atomicAdd(qstats, 1ull);
+                const int slot = atomicAdd(ovf_ctl, 1);
+                if (slot < n) ovf_list[slot] = e0;
+              }
             }
             break;
           }
@@ -1366,15 +1417,17 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
           f = w_flag_poll(flags + e0);
         }
         s_flag = f;
+        s_from = fr;
       }
       SYNC();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* payload loads are sc1: keep them below */
       if (__builtin_amdgcn_readfirstlane(s_flag) == bailed) continue;
+      from = __builtin_amdgcn_readfirstlane(s_from);
     }
 #ifdef UR3E_WAVE_TRACE
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, sub, sub + 1, mid);
+    const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, from, sub + 1, mid);
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const int e = __builtin_amdgcn_readfirstlane(o.e); /* = e0, reloaded from LDS (see WOut::e) */
     if (r == W_BAIL) {
@@ -1413,9 +1466,9 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
   if (tid == 0) {
     __threadfence();
     if (atomicAdd(qctl + W_NQUEUE, 1) == (int)gridDim.x - 1) {
-      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl + k, k < nq ? (int)gridDim.x / nq : 0);
+      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl + k, k < nq ? nstat : 0);
       atomicExch(qctl + W_NQUEUE, 0);
-      atomicExch(qctl + W_NQUEUE + 1, (E + 1) & 0x7ffffff);
+      atomicExch(qctl + W_NQUEUE + 1, E >= 0x7ffffff ? 1 : E + 1); /* never 0: zeroed flags are unclaimed */
     }
   }
 }
@@ -1587,7 +1640,9 @@ struct ur3e_batch {
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
   int* d_ovf_list;
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
-  unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier */
+  unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier,
+                                      [2] routed to the grasp tier, [3] queue give-ups, [4] static
+                                      queue units claimed by their consumer */
   int grasp;       /* the tiers are compact -> grasp (KSG_NV) -> full capacity (main.xml only) */
   int* h_routed;   /* host-mapped routed-env count of the last route snapshot (KState.routed_host) */
   int g_grid;      /* resident workgroups of the grasp-tier list kernel */
@@ -1762,6 +1817,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.np_lanes = cfg->np_chunk_lanes > 0 && cfg->np_chunk_lanes < W_NP_LANES ? cfg->np_chunk_lanes : W_NP_LANES;
   c.obs_sites = model->id_site_tcp >= 0 && model->id_site_handle >= 0 && model->id_body_ghost >= 0;
   c.sensors = cfg->sensors != 0;
+  c.spin_limit = 0;
+  c.leave_static = 0;
   KPlan plan;
   build_plan(model, &plan);
   b->main_tree = model->nv == UR3E_MAIN_NV && plan.max_jntnum <= 1;
@@ -1807,7 +1864,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.nwarn, 0, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_list, sizeof(int) * nd));
   HIPCHK(hipMalloc(&b->d_ovf_ctl, 2 * sizeof(int)));
-  HIPCHK(hipMalloc(&b->d_ovf_total, 3 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&b->d_ovf_total, W_NTOTAL * sizeof(unsigned long long)));
   HIPCHK(hipMemset(b->d_ovf_ctl, 0, 2 * sizeof(int)));
   /* grasp tier between the compact and the full-capacity tier (main.xml's specialised kernels) */
   b->grasp = tiered && b->main_tree;
@@ -1846,7 +1903,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   }
   /* substep work queue: gym tasks with several substeps per env-step on main.xml's compact tier
      (cfg->schedule 1 keeps one workgroup per env-step) */
-  b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 && cfg->schedule != 1;
+  b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 &&
+              c.frame_skip < W_FLAG_CLAIMED && cfg->schedule != 1; /* flag codes: substeps done < 14 */
   b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->q_grid = 0;
   if (b->queued) {
     int per_cu = 0, cus = 0;
@@ -1868,7 +1926,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     int qinit[W_NQUEUE + 2] = {0};
     /* each queue's counter starts past the workgroups' static first units (w_env_step_q) */
     const int nq = (n_envs & 7) ? 1 : W_NQUEUE;
-    for (int k = 0; k < nq; k++) qinit[k] = b->q_grid / nq;
+    const int nstat = b->q_grid / nq < n_envs / nq ? b->q_grid / nq : n_envs / nq; /* substep-0 units */
+    for (int k = 0; k < nq; k++) qinit[k] = nstat;
     qinit[W_NQUEUE + 1] = 1; /* epoch */
     HIPCHK(hipMalloc(&b->d_qctl, sizeof(qinit)));
     HIPCHK(hipMemcpy(b->d_qctl, qinit, sizeof(qinit), hipMemcpyHostToDevice));
@@ -1876,7 +1935,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMemset(b->d_flags, 0, sizeof(int) * nd));
     HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
   }
-  HIPCHK(hipMemset(b->d_ovf_total, 0, 3 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(b->d_ovf_total, 0, W_NTOTAL * sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
   HIPCHK(hipEventCreate(&b->ev1));
   /* qpos0 / zero state; like a gymnasium Env, call ur3e_batch_reset before the first step */
@@ -1994,11 +2053,12 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
         hipLaunchKernelGGL((w_env_step_q<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), 0, st,
                            b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
                            d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
-                           b->d_mid);
+                           b->d_mid, b->d_ovf_total + 3);
       else
         hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                            b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                           d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid);
+                           d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
+                           b->d_ovf_total + 3);
     } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
       hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), 0, st, b->d_model,
                          b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
@@ -2234,6 +2294,21 @@ extern "C" int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* count
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(counts, b->d_ovf_total, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_queue_stats(ur3e_batch_t* b, unsigned long long* stats) {
+  if (!b || !stats) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(stats, b->d_ovf_total + 3, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int leave_static_units) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  b->cfg.spin_limit = spin_limit;
+  b->cfg.leave_static = leave_static_units != 0;
   return UR3E_OK;
 }
 

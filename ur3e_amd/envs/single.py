@@ -21,8 +21,8 @@ class SingleEnv:
     metadata = {"render_modes": ["human", "rgb_array", "depth_array"], "render_fps": 500}
     ENV_ID = None
 
-    def __init__(self, render_mode=None, device: int = 0, seed: int = 0):
-        s = spec(self.ENV_ID)
+    def __init__(self, render_mode=None, device: int = 0, seed: int = 0, config_yaml_path: str | None = None):
+        s = spec(self.ENV_ID, config_yaml_path)
         self._spec = s
         self.render_mode = render_mode
         self.observation_space = Box(low=-np.inf, high=np.inf, shape=(s["obs_dim"],), dtype=np.float64)

@@ -9,6 +9,10 @@ episode cap and controller gains the reference env uses:
 | imitation_indirect-v0 | imitation_env_indirect.py | IMIT_INDIRECT | 24 | v2 Box (:53-54) | 1 | 2500 (before t+=1) | config_l_mug.yml |
 | imitation_direct-v0 | imitation_env_direct.py | IMIT_DIRECT | 13 | actuator ctrlrange (:56-58) | 2 | 1200 (before t+=1) | unused |
 | ur3e-v2 | ur3e_env2.py | GYM_V2 | 24 | v2 Box (:57-64) | 2 | 2500 (after t+=1) | config_l_mug.yml |
+
+config_l_mug.yml is read when the spec is built (as the reference reads it in each env's __init__,
+ur3e_env2.py:66-68), through ur3e_amd.gains: an explicit path, else controller/config/ under the working
+directory, else the packaged copy.
 """
 from __future__ import annotations
 
@@ -40,11 +44,14 @@ def _specs():
     }
 
 
-def spec(env_id: str) -> dict:
+def spec(env_id: str, config_yaml_path: str | None = None) -> dict:
     s = _specs()
     if env_id not in s:
         raise KeyError(env_id)
     d = dict(s[env_id])
+    if d["gains"] is not None and env_id != "gymnasium_env/ur3e-v0":  # v0's gains are hard-coded (ur3e_env.py:49-55)
+        from .. import gains
+        d["gains"] = gains.task_gains(config_yaml_path)
     if d["low"] is None:  # direct torque control: Box = actuator ctrlrange (get_ctrl_ranges)
         from .. import runtime as rt
         md, _ = rt.load_model("main")

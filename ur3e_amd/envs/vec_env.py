@@ -28,10 +28,10 @@ except Exception:  # pragma: no cover
 
 
 def _default_stepper(env_id: str, num_envs: int, device: int, seed: int, env_id_offset: int, envs_per_block: int,
-                     max_episode_steps: int | None):
+                     max_episode_steps: int | None, config_yaml_path: str | None = None):
     """The product stepper: num_envs envs of `env_id` resident on GPU `device` (runtime.Batch)."""
     from .. import runtime as rt
-    s = spec(env_id)
+    s = spec(env_id, config_yaml_path)
     md, mc = rt.load_model("main")
     T = s["T"] if max_episode_steps is None else max_episode_steps
     cfg = rt.make_config(task=s["task"], frame_skip=s["frame_skip"], max_episode_steps=T, model=md, seed=seed,
@@ -42,7 +42,7 @@ def _default_stepper(env_id: str, num_envs: int, device: int, seed: int, env_id_
 class UR3eVecEnv(_SB3VecEnv):
     def __init__(self, num_envs: int = 4096, device: int = 0, seed: int = 0, stepper=None, env_id_offset: int = 0,
                  envs_per_block: int = 0, max_episode_steps: int | None = None,
-                 env_id: str = "gymnasium_env/ur3e-v2", render_mode=None):
+                 env_id: str = "gymnasium_env/ur3e-v2", render_mode=None, config_yaml_path: str | None = None):
         """`render_mode` is accepted for env_kwargs compatibility (train_rl.py:41 passes "human" when
         config_rl.yml:14 visualize is True) and ignored: rendering is out of scope."""
         s = spec(env_id)
@@ -53,7 +53,7 @@ class UR3eVecEnv(_SB3VecEnv):
         self.render_mode = None
         if stepper is None:
             stepper = _default_stepper(env_id, num_envs, device, seed, env_id_offset, envs_per_block,
-                                       max_episode_steps)
+                                       max_episode_steps, config_yaml_path)
         if _SB3VecEnv is not object:  # pragma: no cover - SB3 is not installed in this image
             try:  # SB3 2.x: num_envs, spaces, reset_infos, _seeds/_options, render_mode, metadata
                 _SB3VecEnv.__init__(self, num_envs, self.observation_space, self.action_space)

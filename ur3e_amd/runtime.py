@@ -39,6 +39,7 @@ GAINS_L_POS = dict(kp=[20.0, 60.0, 20.0, 20.0, 20.0, 10.0], kd=[5.0, 15.0, 5.0, 
 GAINS_L_ROT = dict(kp=[5.02, 5.01, 5.80, 5.80, 5.09, 5.80], kd=[5.0, 50.0, 10.0, 5.0, 5.0, 5.0])
 
 _lib = None
+_libs = {}  # other builds of the library loaded side by side (diagnostic variants), by path
 
 
 class ConfigC(ctypes.Structure):
@@ -52,14 +53,26 @@ class ConfigC(ctypes.Structure):
     ]
 
 
-def load_library():
-    """Load the in-tree HIP library; raise loudly when it is absent."""
+def load_library(path: str | None = None):
+    """Load the in-tree HIP library (or, given `path`, another build of it, e.g. a diagnostic variant,
+    side by side with the product library); raise loudly when it is absent."""
     global _lib
+    if path is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        path = os.path.abspath(path)
+        if path not in _libs:
+            if not os.path.exists(path):
+                raise RuntimeError(f"MI355X library variant missing: {path}")
+            _libs[path] = _bind(ctypes.CDLL(path))
+        return _libs[path]
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"MI355X library missing: {LIB_PATH} (run __graft_entry__.build())")
-    L = ctypes.CDLL(LIB_PATH)
+    _lib = _bind(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def _bind(L):
     vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
     L.ur3e_last_error.restype = ctypes.c_char_p
     L.ur3e_batch_create.argtypes = [vp, vp, ip, ip, ctypes.POINTER(vp)]
@@ -77,17 +90,19 @@ def load_library():
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_sensordata.argtypes = [vp, vp, vp]
+    L.ur3e_batch_queue_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ur3e_batch_set_queue_debug.argtypes = [vp, ctypes.c_uint, ip]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim",
               "ur3e_batch_schedule"):
         getattr(L, f).argtypes = [vp]
-    _lib = L
     del dp
     return L
 
 
-def _check(rc):
+def _check(rc, L=None):
     if rc != 0:
-        raise RuntimeError(f"ur3e library error {rc}: {_lib.ur3e_last_error().decode()}")
+        L = L or _lib
+        raise RuntimeError(f"ur3e library error {rc}: {L.ur3e_last_error().decode()}")
 
 
 def load_model(name: str = "main"):
@@ -147,12 +162,12 @@ def _ptr(t):
 class Batch:
     """N UR3e environments on one GPU (C ABI handle + device tensors)."""
 
-    def __init__(self, model_c: UR3eModelC, cfg: ConfigC, n_envs: int, device: int = 0):
+    def __init__(self, model_c: UR3eModelC, cfg: ConfigC, n_envs: int, device: int = 0, lib: str | None = None):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("ur3e_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.torch = torch
-        self.L = load_library()
+        self.L = load_library(lib)
         self.device = torch.device("cuda", device)
         self.model_c = model_c
         self.cfg = cfg
@@ -160,7 +175,7 @@ class Batch:
         self.nq, self.nv, self.nu = model_c.nq, model_c.nv, model_c.nu
         h = ctypes.c_void_p()
         torch.cuda.set_device(self.device)
-        _check(self.L.ur3e_batch_create(ctypes.byref(model_c), ctypes.byref(cfg), n_envs, device, ctypes.byref(h)))
+        self._chk(self.L.ur3e_batch_create(ctypes.byref(model_c), ctypes.byref(cfg), n_envs, device, ctypes.byref(h)))
         self.h = h
         f64 = dict(dtype=torch.float64, device=self.device)
         self.obs_dim = self.L.ur3e_batch_obs_dim(h)
@@ -171,6 +186,9 @@ class Batch:
         self.truncated = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
         self.terminal_obs = torch.zeros((n_envs, self.obs_dim), **f64)
         self.reset()
+
+    def _chk(self, rc):
+        _check(rc, self.L)
 
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -190,12 +208,12 @@ class Batch:
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
-        _check(self.L.ur3e_batch_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()))
+        self._chk(self.L.ur3e_batch_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()))
         return self.obs
 
     def step(self, actions):
         a = actions.to(device=self.device, dtype=self.torch.float64).contiguous()
-        _check(self.L.ur3e_batch_step(self.h, _ptr(a), a.shape[1], _ptr(self.obs), _ptr(self.reward),
+        self._chk(self.L.ur3e_batch_step(self.h, _ptr(a), a.shape[1], _ptr(self.obs), _ptr(self.reward),
                                       _ptr(self.terminated), _ptr(self.truncated), _ptr(self.terminal_obs),
                                       self._stream()))
         return self.obs, self.reward, self.terminated, self.truncated, self.terminal_obs
@@ -205,7 +223,7 @@ class Batch:
         qp = t.empty((self.n, self.nq), dtype=t.float64, device=self.device)
         qv = t.empty((self.n, self.nv), dtype=t.float64, device=self.device)
         wa = t.empty((self.n, self.nv), dtype=t.float64, device=self.device)
-        _check(self.L.ur3e_batch_get_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
+        self._chk(self.L.ur3e_batch_get_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
         return qp, qv, wa
 
     def set_state(self, qpos, qvel, warm=None):
@@ -213,7 +231,7 @@ class Batch:
         qp = t.as_tensor(qpos, dtype=t.float64).to(self.device).contiguous()
         qv = t.as_tensor(qvel, dtype=t.float64).to(self.device).contiguous()
         wa = None if warm is None else t.as_tensor(warm, dtype=t.float64).to(self.device).contiguous()
-        _check(self.L.ur3e_batch_set_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
+        self._chk(self.L.ur3e_batch_set_state(self.h, _ptr(qp), _ptr(qv), _ptr(wa), self._stream()))
 
     def get_info(self):
         t = self.torch
@@ -221,13 +239,13 @@ class Batch:
         el = t.empty(self.n, dtype=t.int32, device=self.device)
         er = t.empty(self.n, dtype=t.float64, device=self.device)
         nw = t.empty(self.n, dtype=t.int32, device=self.device)
-        _check(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
+        self._chk(self.L.ur3e_batch_get_info(self.h, _ptr(nc), _ptr(el), _ptr(er), _ptr(nw), self._stream()))
         return dict(ncon=nc, ep_len=el, ep_return=er, nwarn=nw)
 
     def get_ctrl(self):
         """[N, nu] d.ctrl applied by the last step."""
         out = self.torch.empty((self.n, self.nu), dtype=self.torch.float64, device=self.device)
-        _check(self.L.ur3e_batch_get_ctrl(self.h, _ptr(out), self._stream()))
+        self._chk(self.L.ur3e_batch_get_ctrl(self.h, _ptr(out), self._stream()))
         return out
 
     def get_sensordata(self):
@@ -235,13 +253,13 @@ class Batch:
         sensor declaration order (sensor_names / sensor_adr of the model dict)"""
         nsd = self.model_c.nsensordata
         out = self.torch.zeros((self.n, max(nsd, 1)), dtype=self.torch.float64, device=self.device)
-        _check(self.L.ur3e_batch_get_sensordata(self.h, _ptr(out), self._stream()))
+        self._chk(self.L.ur3e_batch_get_sensordata(self.h, _ptr(out), self._stream()))
         return out[:, :nsd]
 
     def get_carry(self):
         """[N, 54] stale-kinematics snapshot: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6]."""
         out = self.torch.empty((self.n, 54), dtype=self.torch.float64, device=self.device)
-        _check(self.L.ur3e_batch_get_carry(self.h, _ptr(out), self._stream()))
+        self._chk(self.L.ur3e_batch_get_carry(self.h, _ptr(out), self._stream()))
         return out
 
     def touch_index(self, side: str) -> int:
@@ -256,20 +274,32 @@ class Batch:
         """Touch sensors [N, ntouch] after the last forward (mjSENS_TOUCH on the pad sites)."""
         nt = max(self.model_c.ntouch, 1)
         out = self.torch.zeros((self.n, nt), dtype=self.torch.float64, device=self.device)
-        _check(self.L.ur3e_batch_get_touch(self.h, _ptr(out), self._stream()))
+        self._chk(self.L.ur3e_batch_get_touch(self.h, _ptr(out), self._stream()))
         return out[:, :self.model_c.ntouch]
 
     def tier_counts(self) -> tuple:
         """Since create: (env-steps the compact tier handed to the grasp tier, env-steps the grasp tier
         handed to the full-capacity tier, env-steps routed straight to the grasp tier)."""
         v = (ctypes.c_ulonglong * 3)()
-        _check(self.L.ur3e_batch_tier_counts(self.h, v))
+        self._chk(self.L.ur3e_batch_tier_counts(self.h, v))
         return int(v[0]), int(v[1]), int(v[2])
+
+    def queue_stats(self) -> tuple:
+        """Since create, substep work queue: (units that gave up waiting for their producer, static first
+        units claimed and run by their consumer)."""
+        v = (ctypes.c_ulonglong * 2)()
+        self._chk(self.L.ur3e_batch_queue_stats(self.h, v))
+        return int(v[0]), int(v[1])
+
+    def set_queue_debug(self, spin_limit: int = 0, leave_static_units: bool = False):
+        """Diagnostics of the substep queue: flag polls before a waiting unit gives up (0 = built-in
+        bound); leave_static_units: workgroups skip their static first units (consumers claim them)."""
+        self._chk(self.L.ur3e_batch_set_queue_debug(self.h, int(spin_limit), int(leave_static_units)))
 
     def overflow_count(self) -> int:
         """Env-steps the compact tier handed to the full-capacity tier since create."""
         v = ctypes.c_ulonglong()
-        _check(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
+        self._chk(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
         return int(v.value)
 
     SCHEDULES = {0: "w_env_step<64,KSS_NV> (compact tier, one workgroup per env-step)",
@@ -279,17 +309,17 @@ class Batch:
     def kernel_info(self) -> dict:
         """{envs_per_cu, lds_bytes, regs, kernel} of the step kernel this handle launches"""
         e, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        _check(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
+        self._chk(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
         return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value,
                 "kernel": self.SCHEDULES.get(self.L.ur3e_batch_schedule(self.h), "?")}
 
     def set_timing(self, on: bool = True):
         """Record HIP events around every (uncaptured) step, for last_step_ms()."""
-        _check(self.L.ur3e_batch_set_timing(self.h, int(on)))
+        self._chk(self.L.ur3e_batch_set_timing(self.h, int(on)))
 
     def last_step_ms(self) -> float:
         ms = ctypes.c_float()
-        _check(self.L.ur3e_batch_last_step_ms(self.h, ctypes.byref(ms)))
+        self._chk(self.L.ur3e_batch_last_step_ms(self.h, ctypes.byref(ms)))
         return ms.value
 
 
