@@ -198,6 +198,30 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
                                  "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot,
                                  "full_tier_frac": tc[1] / tot}
     drv.close()
+    # C3 as the reference's loop runs it (controller/move_l_mug.py:67-81): the same rows, and after every
+    # mj_step traj_true[t] = get_task_space_state and actuator_frc[t] = get_jnt_torques recorded into
+    # device buffers [rows, N, 7] (two small kernels per row on the same stream)
+    from ur3e_amd.controller.move_l_mug import task_space_state
+    drv = MoveLMug(n_envs, reset_mode="low", seed=0)
+    for t in range(g0):
+        drv.batch.step(drv.traj.row(t))
+    it = iter(rows)
+    tt = torch.empty((steps_c3, n_envs, 7), dtype=torch.float64, device=drv.batch.device)
+    af = torch.empty((steps_c3, n_envs, drv.batch.nu), dtype=torch.float64, device=drv.batch.device)
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(steps_c3):
+        drv.batch.step(next(it))
+        task_space_state(drv.batch, tt[i])
+        drv.batch.get_actuator_force(af[i])
+    e1.record()
+    torch.cuda.synchronize()
+    out["C3_main_move_l_mug_recording"] = {
+        "value": n_envs * steps_c3 / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s", "envs": n_envs,
+        "substeps_per_env_step": 1, "rows": [g0, g1],
+        "records": "traj_true [rows, N, 7] and actuator_frc [rows, N, 7] every row, on the device",
+        "grasp_rows_recorded_frac": float(tt[:, :, 6].mean().item())}
+    drv.close()
     return out
 
 

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 6
+#define UR3E_ABI_VERSION 7
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -160,6 +160,18 @@ int ur3e_batch_get_touch(ur3e_batch_t* b, double* d_touch, void* stream);
    get_jnt_torques (utils/utils.py:201-211, called at controller/move_l_mug.py:80) and
    get_grasp_contact (utils/utils.py:238-245) */
 int ur3e_batch_get_sensordata(ur3e_batch_t* b, double* d_sensordata, void* stream);
+
+/* controller/controller_func.py:191-200 get_task_space_state, as controller/move_l_mug.py:80 records it
+   after every mj_step, d_out [N, 7]: tcp site_xpos (3), tcp rotvec = scipy Rotation.from_matrix(
+   site_xmat).as_rotvec() (utils/utils.py:158-162; 3), and get_boolean_grasp_contact (utils/utils.py:
+   238-245: (left pad touch, right pad touch) > (0.1, 0.1) compared as tuples; 1.0 / 0.0), all of the
+   last step's final forward pass.  Needs main.xml's tcp site and pad touch sensors. */
+int ur3e_batch_get_task_space_state(ur3e_batch_t* b, double* d_out, void* stream);
+
+/* mjData.actuator_force of the last forward, d_out [N, nu]: the actuatorfrc sensors that
+   utils/utils.py:201-211 get_jnt_torques reads (recorded at controller/move_l_mug.py:81), available
+   in every tier (no sensors flag needed).  Not kept by the v1 lane-per-env layout (EINVAL). */
+int ur3e_batch_get_actuator_force(ur3e_batch_t* b, double* d_out, void* stream);
 
 /* d.ctrl after the last step, d_ctrl [N, nu]: the controller output the step applied (pid_task_ctrl
    torques + grip, PD torques, or the raw action); zero after a reset, like mj_resetData.  Replaces the

@@ -130,6 +130,25 @@ class OracleBatch:
             self.L.ur3o_env_sensordata(ctypes.byref(self.m), ptr, _p(out[i]))
         return out[:, :nsd]
 
+    def _env_ptr(self, i):
+        return ctypes.cast(ctypes.addressof(self.buf) + self.L.ur3o_sizeof_env() * i, ctypes.c_void_p)
+
+    def task_space_state(self, touch_left: int, touch_right: int):
+        """[n, 7] controller_func.get_task_space_state of every env's last forward: tcp xpos, tcp rotvec
+        (scipy from_matrix(...).as_rotvec()), boolean grasp contact (touch columns left / right)"""
+        out = np.zeros((self.n, 7))
+        for i in range(self.n):
+            self.L.ur3o_env_task_space_state(ctypes.byref(self.m), self._env_ptr(i), ctypes.c_int(touch_left),
+                                             ctypes.c_int(touch_right), _p(out[i]))
+        return out
+
+    def actuator_force(self):
+        """[n, nu] mjData.actuator_force of every env's last forward (get_jnt_torques)"""
+        out = np.zeros((self.n, self.m.nu))
+        for i in range(self.n):
+            self.L.ur3o_env_actuator_force(ctypes.byref(self.m), self._env_ptr(i), _p(out[i]))
+        return out
+
     def get_ctrl(self):
         """[n, nu] d.ctrl applied by every env's last step"""
         nu = self.m.nu
@@ -173,6 +192,15 @@ def v0_epilogue(model_c, pairs, obs13, act4):
                        _p(np.ascontiguousarray(obs13, dtype=np.float64)),
                        _p(np.ascontiguousarray(act4, dtype=np.float64)), ctypes.byref(r), _p(oi))
     return r.value, int(oi[0]), int(oi[1])
+
+
+def rotvec_from_matrix(xmat):
+    """scipy Rotation.from_matrix(xmat).as_rotvec() as the oracle restates it (utils/utils.py:158-162)"""
+    L = lib()
+    xmat = np.ascontiguousarray(xmat, dtype=np.float64).reshape(9)
+    out = np.zeros(3)
+    L.ur3o_rotvec_from_matrix(_p(xmat), _p(out))
+    return out
 
 
 def rot_err(xmat, target):

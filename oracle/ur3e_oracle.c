@@ -1722,6 +1722,13 @@ void ur3o_rotvec_from_quat(const double qin[4], double rv[3]) {
   rv[0] = sc * q[0]; rv[1] = sc * q[1]; rv[2] = sc * q[2];
 }
 
+/* utils/utils.py:158-162 get_site_xrotvec: R.from_matrix(xmat).as_rotvec() (scipy 1.15.3) */
+void ur3o_rotvec_from_matrix(const double xmat[9], double rv[3]) {
+  double q[4];
+  ur3o_quat_from_matrix(xmat, q);
+  ur3o_rotvec_from_quat(q, rv);
+}
+
 void ur3o_rot_err(const double xmat[9], const double target[3], double err[3]) {
   /* controller_func.py:30-48: q_err = R(target) * R(xmat)^-1 -> rotvec */
   double q[4], qd[4], qi[4], r[4];

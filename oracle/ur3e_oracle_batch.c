@@ -241,6 +241,27 @@ void ur3o_env_sensordata(const ur3e_model_t* m, const ur3o_env* e, double* out) 
   for (int k = 0; k < m->nsensordata; k++) out[k] = e->d.sensordata[k];
 }
 
+/* controller/controller_func.py:191-200 get_task_space_state, read after mj_step (move_l_mug.py:80):
+   tcp site_xpos (3), get_site_xrotvec = scipy from_matrix(site_xmat).as_rotvec() (3), and
+   get_boolean_grasp_contact (utils/utils.py:238-245): the tuple (left pad touch, right pad touch) >
+   (0.1, 0.1), compared lexicographically.  Positions and touch are those of the step's last forward. */
+void ur3o_rotvec_from_matrix(const double xmat[9], double rv[3]);
+void ur3o_env_task_space_state(const ur3e_model_t* m, const ur3o_env* e, int touch_left, int touch_right,
+                               double out[7]) {
+  const ur3o_data* d = &e->d;
+  const int st = m->id_site_tcp;
+  for (int k = 0; k < 3; k++) out[k] = d->site_xpos[st][k];
+  ur3o_rotvec_from_matrix(d->site_xmat[st], out + 3);
+  const double l = d->touch[touch_left], r = d->touch[touch_right];
+  out[6] = (l > 0.1 || (l == 0.1 && r > 0.1)) ? 1.0 : 0.0;
+}
+
+/* utils/utils.py:201-211 get_jnt_torques: the actuatorfrc sensors, i.e. mjData.actuator_force of the
+   last forward (actuators in declaration order: six arm motors, then the fingers) */
+void ur3o_env_actuator_force(const ur3e_model_t* m, const ur3o_env* e, double* out) {
+  for (int k = 0; k < m->nu; k++) out[k] = e->d.actuator_force[k];
+}
+
 void ur3o_env_ctrl(const ur3o_env* e, double* ctrl) {
   for (int k = 0; k < UR3E_MAXU; k++) ctrl[k] = e->d.ctrl[k];
 }

@@ -1,0 +1,46 @@
+"""GPU: config C3 as the reference runs it (controller/move_l_mug.py:67-81): after every mj_step the
+loop records traj_true[t] = get_task_space_state(m, d) (controller_func.py:191-200: tcp xpos, scipy
+rotvec of the tcp xmat, boolean grasp contact from the pad touch sensors) and actuator_frc[t] =
+get_jnt_torques(d) (utils/utils.py:201-211).  Both are computed on the device in the compact and grasp
+tiers (no sensors flag, no host round trip) and must equal the oracle bit for bit on every row of
+16 envs x 2,600 rows, through the grasp."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_move_l_mug_records_every_row_bit_exact():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.move_l_mug import MoveLMug, task_space_state
+    n, rows = 16, 2600
+    drv = MoveLMug(n, reset_mode="low", seed=5)
+    gb = drv.batch
+    assert gb.kernel_info()["kernel"].startswith("w_env_step<64")  # compact tier (grasp tier behind it)
+    ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n)
+    tl, tr = gb.touch_index("left"), gb.touch_index("right")
+    # the start pose the trajectory is built from is the same record at reset
+    np.testing.assert_array_equal(drv.start.cpu().numpy(), ob.task_space_state(tl, tr))
+    # trajectory rows are pure functions of the per-env endpoints (PickPlaceTorch.row)
+    traj = torch.stack([drv.traj.row(t) for t in range(rows)]).cpu().numpy()
+    tt, af = drv.run(rows, record=True)
+    torch.cuda.synchronize()
+    tt, af = tt.cpu().numpy(), af.cpu().numpy()
+    assert tt.shape == (rows, n, 7) and af.shape == (rows, n, 7)
+    # the oracle steps the same rows (evaluated on the host from the same endpoints)
+    grip = 0
+    for t in range(rows):
+        ob.step(np.ascontiguousarray(traj[t]))
+        np.testing.assert_array_equal(tt[t], ob.task_space_state(tl, tr), err_msg=f"traj_true row {t}")
+        np.testing.assert_array_equal(af[t], ob.actuator_force(), err_msg=f"actuator_frc row {t}")
+        grip += int(tt[t, :, 6].sum())
+    assert grip > 0, "no row recorded a grasp contact"
+    assert np.abs(af[:, :, 6]).max() > 0
+    tc = gb.tier_counts()
+    assert tc[0] + tc[2] > 0, tc  # grasp rows ran in the grasp tier
+    st = task_space_state(gb)
+    np.testing.assert_array_equal(st.cpu().numpy(), tt[-1])
+    drv.close()

@@ -10,9 +10,11 @@ Per env, as the reference's main():
 
 The controller and mj_step run inside the step library (task UR3E_TASK_TRAJ_L, one
 substep per row); trajectory rows are evaluated on the GPU (PickPlaceTorch).  The
-task-space state uses the stale-kinematics carry (tcp site pose of the last forward),
-scipy's matrix -> rotvec conversion (as utils/utils.py:158-162 does), and the pad touch
-sensors compared lexicographically with (0.1, 0.1) (utils/utils.py:238-245).
+task-space state is computed on the device (ur3e_batch_get_task_space_state): the
+stale-kinematics carry (tcp site pose of the last forward), scipy's matrix -> rotvec
+conversion restated (utils/utils.py:158-162), and the pad touch sensors compared
+lexicographically with (0.1, 0.1) (utils/utils.py:238-245); actuator_frc is the
+committed mjData.actuator_force (ur3e_batch_get_actuator_force).
 
 Out of scope: the viewer, CSV/plot logging (controller/aux.py cleanup).
 """
@@ -25,22 +27,13 @@ from .build_traj import PickPlaceTorch
 NOISE = {"deterministic": 0, "high": 1, "med": 2, "low": 3}
 
 
-def task_space_state(batch):
-    """get_task_space_state for all envs: [N, 7] = tcp xpos, tcp rotvec, boolean grasp contact."""
-    import torch
-    from scipy.spatial.transform import Rotation as R
-    carry = batch.get_carry()
-    xpos = carry[:, 0:3]
-    xmat = carry[:, 3:12].cpu().numpy().reshape(-1, 3, 3)
-    rotvec = torch.from_numpy(R.from_matrix(xmat).as_rotvec()).to(carry.device)
-    touch = batch.get_touch()
-    # sensor order follows main.xml <sensor>: right_pad1_contact, left_pad1_contact; get_grasp_contact
-    # returns (left, right)
-    li, ri = batch.touch_index("left"), batch.touch_index("right")
-    left, right = touch[:, li], touch[:, ri]
-    # tuple comparison (left, right) > (0.1, 0.1)
-    grip = (left > 0.1) | ((left == 0.1) & (right > 0.1))
-    return torch.cat([xpos, rotvec, grip.to(torch.float64)[:, None]], dim=1)
+def task_space_state(batch, out=None):
+    """get_task_space_state for all envs: [N, 7] = tcp xpos, tcp rotvec, boolean grasp contact, computed
+    on the device (ur3e_batch_get_task_space_state); `out` may be a row of a recording buffer."""
+    if out is None:
+        return batch.get_task_space_state()
+    batch._chk(batch.L.ur3e_batch_get_task_space_state(batch.h, batch.torch_ptr(out), batch._stream()))
+    return out
 
 
 class MoveLMug:
@@ -48,8 +41,11 @@ class MoveLMug:
 
     def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
                  envs_per_block: int = 0, sensors: bool = False, config_yaml_path: str | None = None):
-        """sensors=True also records mjData.sensordata every row (actuator_frc[t] = get_jnt_torques(d),
-        move_l_mug.py:80), at the cost of the full-capacity kernel (see ur3e_config_t.sensors)."""
+        """sensors=True also keeps the full mjData.sensordata (incl. the torque sensors) readable through
+        batch.get_sensordata() after a step, at the cost of the full-capacity kernel (see
+        ur3e_config_t.sensors).  The reference's per-row records -- traj_true (get_task_space_state) and
+        actuator_frc (get_jnt_torques), move_l_mug.py:80-81 -- need no sensors flag: run(record=True)
+        fills them on the device every row, in every tier."""
         import torch
         from .. import gains
         from .. import runtime as rt
@@ -82,10 +78,23 @@ class MoveLMug:
         self.t += 1
         return row
 
-    def run(self, steps: int | None = None, record_every: int = 0):
-        """Run `steps` rows (default: the whole 7200-row trajectory).  With record_every > 0,
-        returns traj_true samples {t: [N, 7]} taken every record_every steps."""
-        steps = self.T if steps is None else min(steps, self.T - self.t)
+    def run(self, steps: int | None = None, record: bool = False, record_every: int = 0):
+        """Run `steps` rows (default: the rest of the 7200-row trajectory).
+        record=True: as the reference's loop (move_l_mug.py:67-81), every row's traj_true
+        (get_task_space_state after mj_step) and actuator_frc (get_jnt_torques) go into device buffers
+        [steps, N, 7], returned as (traj_true, actuator_frc).  record_every > 0 instead returns
+        traj_true samples {t: [N, 7]} every record_every rows."""
+        torch = self.torch
+        steps = self.T - self.t if steps is None else min(steps, self.T - self.t)
+        if record:
+            dev = self.batch.device
+            traj_true = torch.empty((steps, self.batch.n, 7), dtype=torch.float64, device=dev)
+            act_frc = torch.empty((steps, self.batch.n, self.batch.nu), dtype=torch.float64, device=dev)
+            for i in range(steps):
+                self.step()
+                task_space_state(self.batch, traj_true[i])
+                self.batch.get_actuator_force(act_frc[i])
+            return traj_true, act_frc
         rec = {}
         for _ in range(steps):
             self.step()
@@ -94,14 +103,9 @@ class MoveLMug:
         return rec
 
     def actuator_frc(self):
-        """[N, 7] get_jnt_torques (utils/utils.py:201-211): the 7 actuatorfrc sensors by name order"""
-        md = self.md
-        names = ["shoulder_pan_motor", "shoulder_lift_motor", "elbow_motor", "wrist_1_motor", "wrist_2_motor",
-                 "wrist_3_motor", "fingers_actuator"]
-        act = {nm: k for k, nm in enumerate(md["act_names"])}
-        adr = {md["sensor_objid"][j]: md["sensor_adr"][j] for j in range(md["nsensor"]) if md["sensor_type"][j] == 1}
-        sd = self.batch.get_sensordata()
-        return sd[:, [adr[act[nm]] for nm in names]]
+        """[N, 7] get_jnt_torques (utils/utils.py:201-211): the 7 actuatorfrc sensors in name order
+        (= main.xml's actuator order), i.e. mjData.actuator_force of the last forward"""
+        return self.batch.get_actuator_force()
 
     def close(self):
         self.batch.close()

@@ -386,6 +386,7 @@ struct KState {
   double* touch; /* [env][UR3E_MAXTOUCH] touch sensors after the last forward */
   double* ctrl;  /* [env][UR3E_MAXU] d.ctrl after the last step (the controller output it applied) */
   double* sensordata; /* [env][UR3E_MAXSENSORDATA] mjData.sensordata of the last forward (sensors on) */
+  double* actfrc; /* [env][UR3E_MAXU] mjData.actuator_force of the last forward (workgroup-per-env kernels) */
   /* tier routing (grasp tier on): hint[e] = the env's last committed forward had more than
      W_ROUTE_NCON contacts; route[e] = the snapshot of hint the current step routes by (written only
      between steps, by the last kernel of the step): routed envs skip the compact tier and run in the
@@ -881,7 +882,10 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
   for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
   for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
-  for (int k = tid; k < m->nu; k += NT) st.ctrl[(size_t)e * UR3E_MAXU + k] = s.ctrl[k];
+  for (int k = tid; k < m->nu; k += NT) {
+    st.ctrl[(size_t)e * UR3E_MAXU + k] = s.ctrl[k];
+    st.actfrc[(size_t)e * UR3E_MAXU + k] = s.act_force[k];
+  }
   if constexpr (!KS::OVERLAY) {
     if (c.sensors)
       for (int k = tid; k < m->nsensordata; k += NT)
@@ -1855,6 +1859,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   HIPCHK(hipMemset(s.touch, 0, sizeof(double) * nd * UR3E_MAXTOUCH));
   HIPCHK(hipMalloc(&s.ctrl, sizeof(double) * nd * UR3E_MAXU));
   HIPCHK(hipMemset(s.ctrl, 0, sizeof(double) * nd * UR3E_MAXU));
+  HIPCHK(hipMalloc(&s.actfrc, sizeof(double) * nd * UR3E_MAXU));
+  HIPCHK(hipMemset(s.actfrc, 0, sizeof(double) * nd * UR3E_MAXU));
   s.sensordata = nullptr;
   if (c.sensors) {
     HIPCHK(hipMalloc(&s.sensordata, sizeof(double) * nd * UR3E_MAXSENSORDATA));
@@ -1950,7 +1956,8 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (!b) return UR3E_OK;
   (void)hipSetDevice(b->device);
   void* bufs[] = {b->d_model, b->d_plan, b->st.qpos, b->st.qvel, b->st.warm, b->st.carry, b->st.t, b->st.episode,
-                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->d_ovf_list, b->d_ovf_ctl,
+                  b->st.ep_len, b->st.ep_return, b->st.ncon, b->st.nwarn, b->st.touch, b->st.ctrl, b->st.actfrc,
+                  b->d_ovf_list, b->d_ovf_ctl,
                   b->d_ovf_total};
   for (void* p : bufs) (void)hipFree(p);
   if (b->st.sensordata) (void)hipFree(b->st.sensordata);
@@ -2189,6 +2196,61 @@ extern "C" int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream
   HIPCHK(hipSetDevice(b->device));
   hipLaunchKernelGGL(k_env_get_ctrl, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
                      b->host_model.nu, d_ctrl);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+/* controller/controller_func.py:191-200 get_task_space_state after mj_step: tcp site_xpos, tcp rotvec
+   (scipy from_matrix(site_xmat).as_rotvec(), utils/utils.py:158-162) and get_boolean_grasp_contact
+   ((left pad touch, right pad touch) > (0.1, 0.1) lexicographically, utils/utils.py:238-245), all of
+   the step's last forward: the carry's tcp pose and the committed touch sensors */
+__global__ void k_env_task_space_state(KState s, int tl, int tr, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  double xm[9], q[4], rv[3];
+  double* o = out + (size_t)e * 7;
+  for (int k = 0; k < 3; k++) o[k] = s.carry[SC(s, k, e)];
+  for (int k = 0; k < 9; k++) xm[k] = s.carry[SC(s, 3 + k, e)];
+  k_quat_from_matrix(xm, q);
+  k_rotvec_from_quat(q, rv);
+  for (int k = 0; k < 3; k++) o[3 + k] = rv[k];
+  const double l = s.touch[(size_t)e * UR3E_MAXTOUCH + tl], r = s.touch[(size_t)e * UR3E_MAXTOUCH + tr];
+  o[6] = (l > 0.1 || (l == 0.1 && r > 0.1)) ? 1.0 : 0.0;
+}
+
+__global__ void k_env_get_actfrc(KState s, int nu, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n) return;
+  for (int k = 0; k < nu; k++) out[(size_t)e * nu + k] = s.actfrc[(size_t)e * UR3E_MAXU + k];
+}
+
+/* the touch sensor (column of d_touch) whose site is on body `body`, or -1 */
+static int touch_of_body(const ur3e_model_t* m, int body) {
+  if (body < 0) return -1;
+  for (int k = 0; k < m->ntouch; k++)
+    if (m->site_bodyid[m->touch_site[k]] == body) return k;
+  return -1;
+}
+
+extern "C" int ur3e_batch_get_task_space_state(ur3e_batch_t* b, double* d_out, void* stream) {
+  if (!b || !d_out) return fail(UR3E_EINVAL, "null argument");
+  const ur3e_model_t* m = &b->host_model;
+  const int tl = touch_of_body(m, m->id_body_lpad), tr = touch_of_body(m, m->id_body_rpad);
+  if (m->id_site_tcp < 0 || tl < 0 || tr < 0)
+    return fail(UR3E_EMODEL, "task-space state needs the tcp site and the pad touch sensors (assets/main.xml)");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_task_space_state, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
+                     tl, tr, d_out);
+  HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_get_actuator_force(ur3e_batch_t* b, double* d_out, void* stream) {
+  if (!b || !d_out) return fail(UR3E_EINVAL, "null argument");
+  if (!b->tiered && !b->wave_nt) return fail(UR3E_EINVAL, "the v1 lane-per-env layout does not keep actuator forces");
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(k_env_get_actfrc, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->st,
+                     b->host_model.nu, d_out);
   HIPCHK(hipGetLastError());
   return UR3E_OK;
 }

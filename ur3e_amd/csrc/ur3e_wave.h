@@ -174,6 +174,7 @@ struct KSX<MC, ME, NVC, TREE, true> {
   int con_geom1[MC], con_geom2[MC], con_cpair[MC], con_efc[MC];
   double touch[UR3E_MAXTOUCH];
   double eq_p[UR3E_MAXEQ][6];  /* connect anchors p1, p2 in world coordinates */
+  double act_force[K_NU];      /* mjData.actuator_force of the last forward (committed: get_jnt_torques) */
   double site_vel[2][6];       /* [tcp, handle] mj_objectVelocity (world, [w, v]) */
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
   int bdiag; /* static tree: no constraint row couples the two dof trees (set by r_mc_rows) */
@@ -195,7 +196,7 @@ struct KSX<MC, ME, NVC, TREE, true> {
         };
         struct { /* KB */
           double cinert[K_NB][10], cdof_dot[K_NV][6], cvel[K_NB][6];
-          double actuator_length[K_NU], act_force[K_NU], qfrc_passive[K_NV];
+          double actuator_length[K_NU], qfrc_passive[K_NV];
           union {
             struct {
               double b10[K_NB][10];

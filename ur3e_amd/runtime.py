@@ -90,6 +90,8 @@ def _bind(L):
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_sensordata.argtypes = [vp, vp, vp]
+    L.ur3e_batch_get_task_space_state.argtypes = [vp, vp, vp]
+    L.ur3e_batch_get_actuator_force.argtypes = [vp, vp, vp]
     L.ur3e_batch_queue_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_set_queue_debug.argtypes = [vp, ctypes.c_uint, ip]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim",
@@ -187,6 +189,12 @@ class Batch:
         self.terminal_obs = torch.zeros((n_envs, self.obs_dim), **f64)
         self.reset()
 
+    @staticmethod
+    def torch_ptr(t):
+        """device pointer of a contiguous tensor (or a contiguous row view of one)"""
+        assert t.is_contiguous()
+        return _ptr(t)
+
     def _chk(self, rc):
         _check(rc, self.L)
 
@@ -255,6 +263,21 @@ class Batch:
         out = self.torch.zeros((self.n, max(nsd, 1)), dtype=self.torch.float64, device=self.device)
         self._chk(self.L.ur3e_batch_get_sensordata(self.h, _ptr(out), self._stream()))
         return out[:, :nsd]
+
+    def get_task_space_state(self):
+        """[N, 7] controller_func.get_task_space_state of the last step: tcp xpos, tcp rotvec (scipy
+        from_matrix(...).as_rotvec() restated), boolean grasp contact -- computed on the device"""
+        out = self.torch.empty((self.n, 7), dtype=self.torch.float64, device=self.device)
+        self._chk(self.L.ur3e_batch_get_task_space_state(self.h, _ptr(out), self._stream()))
+        return out
+
+    def get_actuator_force(self, out=None):
+        """[N, nu] mjData.actuator_force of the last forward (get_jnt_torques); `out` may be a row view
+        of a recording buffer"""
+        if out is None:
+            out = self.torch.empty((self.n, self.nu), dtype=self.torch.float64, device=self.device)
+        self._chk(self.L.ur3e_batch_get_actuator_force(self.h, _ptr(out), self._stream()))
+        return out
 
     def get_carry(self):
         """[N, 54] stale-kinematics snapshot: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6]."""
