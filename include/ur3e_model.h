@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define UR3E_MODEL_VERSION 5
+#define UR3E_MODEL_VERSION 6
 
 #define UR3E_MAXBODY 28
 #define UR3E_MAXJNT 16
@@ -37,6 +37,8 @@ extern "C" {
 #define UR3E_MAXTOUCH 4
 #define UR3E_MAXSENSOR 16
 #define UR3E_MAXSENSORDATA 48
+#define UR3E_MAXMESH 16       /* convex mesh geoms' meshes */
+#define UR3E_MAXMESHVERT 1024 /* hull vertices of all meshes */
 
 /* per-env dynamic capacities (the kernels size scratch from these) */
 #define UR3E_MAXCON 40                                   /* contacts per env (main.xml: nconmax 100) */
@@ -52,6 +54,7 @@ extern "C" {
 /* geom types (MuJoCo numbering for the ones used) */
 #define UR3E_GEOM_PLANE 0
 #define UR3E_GEOM_BOX 6
+#define UR3E_GEOM_MESH 7 /* convex hull of a mesh asset (real meshes; see ur3e_amd/model/mesh.py) */
 
 /* equality types */
 #define UR3E_EQ_CONNECT 0
@@ -213,6 +216,14 @@ typedef struct ur3e_model_t {
   int sensor_type[UR3E_MAXSENSOR];
   int sensor_objid[UR3E_MAXSENSOR]; /* site (touch, torque) or actuator (actuatorfrc) */
   int sensor_adr[UR3E_MAXSENSOR];
+  /* convex mesh geoms (geom_type UR3E_GEOM_MESH, compiled when the MJCF's mesh files exist): each
+     mesh's convex-hull vertices in its geom frame, which is the mesh's inertial frame (MuJoCo
+     re-expresses a mesh about its centre of mass and principal axes); geom_dataid = mesh index */
+  int nmesh, nmeshvert;
+  int geom_dataid[UR3E_MAXGEOM];
+  int mesh_vertadr[UR3E_MAXMESH];
+  int mesh_vertnum[UR3E_MAXMESH];
+  double mesh_vert[UR3E_MAXMESHVERT][3];
 } ur3e_model_t;
 
 #ifdef __cplusplus

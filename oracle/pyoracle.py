@@ -90,6 +90,16 @@ class OracleBatch:
         self.L.ur3o_batch_init(ctypes.byref(self.m), ctypes.byref(self.cfg), ctypes.c_int(n_envs), self.buf,
                                _p(self.obs))
 
+    def reset_all(self):
+        """reset every env again (a new episode: fresh reset noise), as ur3e_batch_reset(mask=None)"""
+        obs = np.zeros((self.n, self.od))
+        sz = self.L.ur3o_sizeof_env()
+        for i in range(self.n):
+            ptr = ctypes.cast(ctypes.addressof(self.buf) + sz * i, ctypes.c_void_p)
+            self.L.ur3o_batch_reset_one(ctypes.byref(self.m), ctypes.byref(self.cfg), ptr, _p(obs[i]))
+        self.obs = obs
+        return obs
+
     def step(self, actions: np.ndarray):
         actions = np.ascontiguousarray(actions, dtype=np.float64)
         n = self.n

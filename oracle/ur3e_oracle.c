@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include "../ur3e_amd/csrc/detmath.h"
+#include "../ur3e_amd/csrc/convex.h"
 
 #define MINVAL 1e-15
 #define MINIMP 0.0001
@@ -656,6 +657,41 @@ static int box_box(const double p1[3], const double R1[9], const double s1[3], c
   return cnt;
 }
 
+/* a geom as a convex shape: box (half sizes) or the hull of its mesh, at its current pose */
+static void geom_convex(const ur3e_model_t* m, const ur3o_data* d, int g, ur3e_cvx* c) {
+  if (m->geom_type[g] == UR3E_GEOM_MESH) {
+    const int id = m->geom_dataid[g];
+    c->v = &m->mesh_vert[m->mesh_vertadr[id]][0];
+    c->nv = m->mesh_vertnum[id];
+  } else {
+    c->v = 0;
+    c->nv = 0;
+  }
+  for (int k = 0; k < 3; k++) { c->size[k] = m->geom_size[g][k]; c->pos[k] = d->geom_xpos[g][k]; }
+  for (int k = 0; k < 9; k++) c->mat[k] = d->geom_xmat[g][k];
+}
+
+/* convex mesh pairs (convex.h): plane-mesh (<= UR3E_CVX_PLANE_MAX contacts), box-mesh and mesh-mesh
+   (GJK + EPA, one contact) */
+static int mesh_collide(const ur3e_model_t* m, const ur3o_data* d, int g1, int g2, double margin, rawcon* out) {
+  ur3e_cvx b;
+  geom_convex(m, d, g2, &b);
+  if (m->geom_type[g1] == UR3E_GEOM_PLANE) {
+    double pos[UR3E_CVX_PLANE_MAX][3], nrm[UR3E_CVX_PLANE_MAX][3], dist[UR3E_CVX_PLANE_MAX];
+    const int n = ur3e_plane_convex(d->geom_xpos[g1], d->geom_xmat[g1], &b, margin, pos, nrm, dist);
+    for (int k = 0; k < n; k++) {
+      memcpy(out[k].pos, pos[k], sizeof(out[k].pos));
+      memcpy(out[k].n, nrm[k], sizeof(out[k].n));
+      out[k].dist = dist[k];
+    }
+    return n;
+  }
+  ur3e_cvx a;
+  geom_convex(m, d, g1, &a);
+  ur3e_epa scratch;
+  return ur3e_convex_convex(&a, &b, margin, &scratch, out[0].pos, out[0].n, &out[0].dist);
+}
+
 static void collision(const ur3e_model_t* m, ur3o_data* d) {
   d->ncon = 0;
   d->con_overflow = 0;
@@ -678,6 +714,8 @@ static void collision(const ur3e_model_t* m, ur3o_data* d) {
     } else if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX) {
       n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], m->geom_size[g1], d->geom_xpos[g2], d->geom_xmat[g2],
                   m->geom_size[g2], margin, raw);
+    } else if (t2 == UR3E_GEOM_MESH) {
+      n = mesh_collide(m, d, g1, g2, margin, raw);
     }
     for (int k = 0; k < n; k++) {
       if (d->ncon >= UR3E_MAXCON) { d->con_overflow = 1; break; }

@@ -57,7 +57,9 @@ def test_ppo_actions_replay_bit_exact():
     algo.learn(iters)
     torch.cuda.synchronize()
     assert len(rec.log) == T * iters
+    # the Batch resets at creation and VecNormalize.reset resets again (a second episode): so does the oracle
     ob = po.OracleBatch(mc, po.config_from(cfg), n)
+    ob.reset_all()
     np.testing.assert_array_equal(rec.obs0, ob.obs)
     ends = 0
     acts = np.stack([r[0] for r in rec.log])

@@ -1788,6 +1788,10 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     return fail(UR3E_EMODEL, "task-space control needs the tcp site");
   if (cfg->reset_key >= model->nkey) return fail(UR3E_EINVAL, "reset_key out of range");
   if (cfg->envs_per_block > 64) return fail(UR3E_EINVAL, "envs_per_block > 64");
+  if (model->nmesh > 0 && cfg->envs_per_block > 0)
+    return fail(UR3E_EINVAL, "convex mesh geoms need a workgroup-per-env layout (envs_per_block <= 0)");
+  if (model->nmesh > UR3E_MAXMESH || model->nmeshvert > UR3E_MAXMESHVERT)
+    return fail(UR3E_EMODEL, "convex meshes exceed the model image capacities");
   /* 0: two-tier (default); -64: full-capacity tier, 64 lanes; other negative: full-capacity tier,
      128 lanes; 1..64: v1 lane-per-env */
   if (cfg->sensors && cfg->envs_per_block > 0)

@@ -27,6 +27,7 @@
 
 #include "../../include/ur3e_model.h"
 #include "detmath.h"
+#include "convex.h"
 
 /* kernel capacities: the largest reference model (main.xml: nq 21, nv 20, 25 bodies) */
 #define K_NQ 21

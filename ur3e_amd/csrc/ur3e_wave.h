@@ -687,12 +687,53 @@ WD bool w_pair_near(KModel m, const KS& s, int p) {
   return true;
 }
 
+/* geom g as a convex shape (convex.h): box half sizes, or its mesh's hull vertices (model image) */
+template <class KS>
+__device__ __forceinline__ void w_geom_convex(KModel m, const KS& s, int g, ur3e_cvx* c) {
+  if (m->geom_type[g] == UR3E_GEOM_MESH) {
+    const int id = m->geom_dataid[g];
+    c->v = &m->mesh_vert[m->mesh_vertadr[id]][0];
+    c->nv = m->mesh_vertnum[id];
+  } else {
+    c->v = nullptr;
+    c->nv = 0;
+  }
+  for (int k = 0; k < 3; k++) { c->size[k] = m->geom_size[g][k]; c->pos[k] = s.geom_xpos[g][k]; }
+  for (int k = 0; k < 9; k++) c->mat[k] = s.geom_xmat[g][k];
+}
+
+/* convex mesh pairs, full-capacity tier only: plane-mesh (<= UR3E_CVX_PLANE_MAX contacts), box-mesh
+   and mesh-mesh (GJK + EPA, one contact); the same convex.h code as the oracle's mesh_collide.  Inlined:
+   the narrowphase runs in a divergent region (one candidate per lane), where an out-of-line call was
+   once miscompiled (r_collision) */
+template <class KS>
+__device__ __forceinline__ int w_mesh_collide(KModel m, const KS& s, int g1, int g2, double margin, KRaw* raw) {
+  ur3e_cvx b;
+  w_geom_convex(m, s, g2, &b);
+  if (m->geom_type[g1] == UR3E_GEOM_PLANE) {
+    double pos[UR3E_CVX_PLANE_MAX][3], nrm[UR3E_CVX_PLANE_MAX][3], dist[UR3E_CVX_PLANE_MAX];
+    const int n = ur3e_plane_convex(s.geom_xpos[g1], s.geom_xmat[g1], &b, margin, pos, nrm, dist);
+    for (int k = 0; k < n; k++) {
+      for (int c = 0; c < 3; c++) { raw[k].pos[c] = pos[k][c]; raw[k].n[c] = nrm[k][c]; }
+      raw[k].dist = dist[k];
+    }
+    return n;
+  }
+  ur3e_cvx a;
+  w_geom_convex(m, s, g1, &a);
+  ur3e_epa scratch;
+  return ur3e_convex_convex(&a, &b, margin, &scratch, raw[0].pos, raw[0].n, &raw[0].dist);
+}
+
 /* narrowphase of candidate pair p (after w_pair_near): raw contacts, returns their count */
 template <class KS, bool INL = false>
 WD int w_narrow_core(KModel m, const KS& s, int p, KRaw* raw) {
   int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  if constexpr (!KS::OVERLAY) {
+    if (t2 == UR3E_GEOM_MESH) return w_mesh_collide(m, s, g1, g2, margin, raw);
+  }
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
     return k_plane_box(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2], margin,
                        raw);
@@ -743,6 +784,12 @@ WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
   double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const KStageEmit<KS::NPST> emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
+  /* convex meshes run in the full-capacity tier: a mesh pair within its bounding spheres hands the
+     env-step on */
+  if (t2 == UR3E_GEOM_MESH) {
+    s.ovf = 1;
+    return 0;
+  }
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
     return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2],
                          margin, emit);

@@ -4,10 +4,13 @@ Replaces `mujoco.MjModel.from_xml_path` (reference `utils/utils.py:9-12`;
 `MujocoEnv.__init__` via `gymnasium_env/envs/ur3e_env2.py:32,50-55`) for exactly
 the MJCF features the three reference models use:
 
-* `<compiler angle="radian" autolimits="true">`, `<option>` (timestep, gravity,
+* `<compiler angle="radian" autolimits="true" meshdir>`, `<option>` (timestep, gravity,
   cone, impratio), `<default>` classes with `class`/`childclass` inheritance;
 * bodies (pos, quat), `<inertial>` (diaginertia + quat), hinge and free joints,
-  geoms (plane, box, mesh -> surrogate box, see `surrogate.py`), sites;
+  geoms (plane, box, mesh), sites.  Mesh geoms: when every `<asset><mesh>` file exists, real convex
+  mesh geoms (`mesh.py`: STL/OBJ, convex hull, MuJoCo's mesh inertia and inertial frame); otherwise
+  -- the reference's case, its meshes are git-ignored -- the documented box surrogate
+  (`surrogate.py`).  `compile_mjcf(path, meshes="auto" | "mesh" | "surrogate")`;
 * `<contact>` `<exclude>` and `<pair>`, fixed tendons, equality connect/joint,
   motor and general(affine) actuators, touch / actuatorfrc / torque sensors, keyframes.
 
@@ -30,6 +33,7 @@ import xml.etree.ElementTree as ET
 
 import numpy as np
 
+from . import mesh as _mesh
 from .surrogate import DENSITY, MESH_SURROGATE
 
 # ---------------------------------------------------------------------------
@@ -38,11 +42,12 @@ MAXBODY, MAXJNT, MAXNQ, MAXNV = 28, 16, 24, 24
 MAXGEOM, MAXSITE, MAXCPAIR, MAXEQ = 32, 20, 320, 4
 MAXU, MAXTEN, MAXTENWRAP, MAXKEY, MAXTOUCH = 8, 2, 4, 2, 4
 MAXSENSOR = 16
-MODEL_VERSION = 5
+MAXMESH, MAXMESHVERT = 16, 1024
+MODEL_VERSION = 6
 SENS_TOUCH, SENS_ACTUATORFRC, SENS_TORQUE = 0, 1, 2
 
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = 0, 1, 2, 3
-GEOM_PLANE, GEOM_BOX = 0, 6
+GEOM_PLANE, GEOM_BOX, GEOM_MESH = 0, 6, 7
 EQ_CONNECT, EQ_JOINT = 0, 2
 TRN_JOINT, TRN_TENDON = 0, 3
 BIAS_NONE, BIAS_AFFINE = 0, 1
@@ -148,12 +153,42 @@ def _attrs(defaults, el, childclass):
 
 
 # ---------------------------------------------------------------------------
-def compile_mjcf(path: str) -> dict:
-    """Compile one reference MJCF file into a model dict."""
+def _mesh_assets(root, defaults, path):
+    """<asset><mesh> entries: name -> {file (resolved against <compiler meshdir>), scale, inertia}"""
+    comp = root.find("compiler")
+    meshdir = comp.get("meshdir", "") if comp is not None else ""
+    base = os.path.join(os.path.dirname(os.path.abspath(path)), meshdir)
+    out = {}
+    asset = root.find("asset")
+    if asset is None:
+        return out
+    for ch in asset:
+        if ch.tag != "mesh":
+            continue
+        a = dict(defaults.resolve("mesh", ch.get("class") or "main"))
+        a.update({k: v for k, v in ch.attrib.items() if k != "class"})
+        f = a["file"]
+        name = a.get("name") or os.path.splitext(os.path.basename(f))[0]
+        out[name] = dict(file=os.path.join(base, f), scale=(_floats(a.get("scale", "1 1 1")) + [1.0] * 3)[:3],
+                         inertia=a.get("inertia", "legacy"))
+    return out
+
+
+def compile_mjcf(path: str, meshes: str = "auto") -> dict:
+    """Compile one MJCF file into a model dict.  meshes: "auto" = real mesh geoms when every mesh file
+    exists, else the box surrogate; "mesh" = real meshes (missing files raise); "surrogate"."""
     tree = ET.parse(path)
     root = tree.getroot()
     defaults = _Defaults(root)
     model_name = os.path.basename(path)
+    if meshes not in ("auto", "mesh", "surrogate"):
+        raise ValueError(f"meshes must be 'auto', 'mesh' or 'surrogate', got {meshes!r}")
+    assets = _mesh_assets(root, defaults, path)
+    missing = [a["file"] for a in assets.values() if not os.path.exists(a["file"])]
+    if meshes == "mesh" and missing:
+        raise FileNotFoundError(f"mesh files missing: {missing}")
+    real_meshes = bool(assets) and not missing and meshes != "surrogate"
+    mesh_cache = {}
 
     comp = root.find("compiler")
     autolimits = comp is not None and comp.get("autolimits", "false") == "true"
@@ -238,7 +273,7 @@ def compile_mjcf(path: str) -> dict:
                 b["joints"].append(len(joints) - 1)
             elif ch.tag == "geom":
                 a = _attrs(defaults, ch, cc)
-                g = _make_geom(a, bid)
+                g = _make_geom(a, bid, assets if real_meshes else None, mesh_cache)
                 if ch.get("name"):
                     names["geom"][ch.get("name")] = len(geoms)
                 g["name"] = ch.get("name")
@@ -527,6 +562,24 @@ def compile_mjcf(path: str) -> dict:
             sens_adr.append(nsd)
             nsd += dim
 
+    # ---------------- convex meshes of the collision geoms: one hull per mesh asset, pooled
+    mesh_names, mesh_adr, mesh_num, mesh_vert = [], [], [], []
+    geom_dataid = []
+    for gi in col:
+        g = geoms[gi]
+        if g["type"] != GEOM_MESH:
+            geom_dataid.append(-1)
+            continue
+        if g["mesh"] not in mesh_names:
+            mesh_names.append(g["mesh"])
+            mesh_adr.append(len(mesh_vert))
+            mesh_num.append(len(g["hull"]))
+            mesh_vert.extend(np.asarray(g["hull"]).tolist())
+        geom_dataid.append(mesh_names.index(g["mesh"]))
+    if len(mesh_names) > MAXMESH or len(mesh_vert) > MAXMESHVERT:
+        raise ValueError(f"convex meshes exceed the model image ({len(mesh_names)} meshes, {len(mesh_vert)} hull "
+                         f"vertices; capacities {MAXMESH}, {MAXMESHVERT})")
+
     # ---------------- keyframes
     keys = {}
     ke = root.find("keyframe")
@@ -592,6 +645,8 @@ def compile_mjcf(path: str) -> dict:
         key_names=key_names,
         key_qpos=[keys[k][0].tolist() for k in key_names], key_qvel=[keys[k][1].tolist() for k in key_names],
         body_names=[b["name"] for b in bodies], joint_names=[j["name"] for j in joints],
+        nmesh=len(mesh_names), nmeshvert=len(mesh_vert), geom_dataid=geom_dataid, mesh_vertadr=mesh_adr,
+        mesh_vertnum=mesh_num, mesh_vert=mesh_vert, mesh_names=mesh_names,
     )
 
     def _nid(kind, nm):
@@ -643,13 +698,46 @@ def _pad_solimp(v):
     return v[:5]
 
 
-def _make_geom(a, bid):
+def _load_convex(asset, cache):
+    """mesh asset -> hull vertices in the mesh's inertial frame, unit-density volume and principal
+    inertia, and that frame (com, rotation) in mesh coordinates (mjCMesh processing)"""
+    key = asset["file"], tuple(asset["scale"]), asset["inertia"]
+    if key not in cache:
+        v, f = _mesh.load_mesh(asset["file"], asset["scale"])
+        hidx, _ = _mesh.convex_hull(v)
+        vol, com, I = _mesh.mesh_inertia(v, f, asset["inertia"])
+        w, Rp = _mesh.principal_frame(I)
+        hull = (v[hidx] - com) @ Rp  # coordinates along the principal axes
+        cache[key] = dict(hull=hull, vol=vol, inertia=w, com=com, R=Rp)
+    return cache[key]
+
+
+def _make_geom(a, bid, mesh_assets=None, mesh_cache=None):
     gtype = a.get("type", "sphere")
     pos = np.array(_floats(a.get("pos", "0 0 0")))
     quat = qnorm(_floats(a.get("quat", "1 0 0 0")))
     contype = int(a.get("contype", 1))
     conaffinity = int(a.get("conaffinity", 1))
     surrogate = 0
+    if gtype == "mesh" and mesh_assets is not None:
+        cv = _load_convex(mesh_assets[a["mesh"]], mesh_cache)
+        # the geom frame moves to the mesh's inertial frame (MuJoCo re-centres and re-aligns meshes)
+        pos = pos + q2mat(quat) @ cv["com"]
+        quat = qnorm(qmul(quat, mat2q(cv["R"])))
+        hull = cv["hull"]
+        size = list(np.max(np.abs(hull), axis=0))
+        fr = _floats(a["friction"]) if "friction" in a else list(DEF_FRICTION)
+        fr = (fr + list(DEF_FRICTION[len(fr):]))[:3]
+        vol = cv["vol"]
+        mass = float(a["mass"]) if "mass" in a else DENSITY * vol
+        return dict(type=GEOM_MESH, body=bid, pos=pos, quat=quat, size=size, contype=contype,
+                    conaffinity=conaffinity, condim=int(a.get("condim", 3)), priority=int(a.get("priority", 0)),
+                    friction=fr, solref=_floats(a["solref"]) if "solref" in a else list(DEF_SOLREF),
+                    solimp=_pad_solimp(_floats(a["solimp"])) if "solimp" in a else list(DEF_SOLIMP),
+                    margin=float(a.get("margin", 0.0)), gap=float(a.get("gap", 0.0)),
+                    solmix=float(a.get("solmix", 1.0)), mass=mass,
+                    rbound=float(np.max(np.linalg.norm(hull, axis=1))), surrogate=0,
+                    mesh=a["mesh"], hull=hull, inertia_diag=np.asarray(cv["inertia"]) * (mass / vol))
     if gtype == "mesh":
         half, center, collide = MESH_SURROGATE[a["mesh"]]
         pos = pos + q2mat(quat) @ np.array(center)
@@ -694,7 +782,10 @@ def _inertia_from_geoms(gs):
     for g in gs:
         a, b, c = g["size"]
         m = g["mass"]
-        Ig = np.diag([m / 3 * (b * b + c * c), m / 3 * (a * a + c * c), m / 3 * (a * a + b * b)])
+        if g["type"] == GEOM_MESH:  # principal inertia of the mesh solid, in the geom (inertial) frame
+            Ig = np.diag(g["inertia_diag"])
+        else:
+            Ig = np.diag([m / 3 * (b * b + c * c), m / 3 * (a * a + c * c), m / 3 * (a * a + b * b)])
         R = q2mat(g["quat"])
         d = g["pos"] - com
         I += R @ Ig @ R.T + m * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
@@ -933,7 +1024,13 @@ class UR3eModelC(ctypes.Structure):
         ("fish_half_z", _d),
         ("nsensor", _i), ("nsensordata", _i), ("sensor_type", _i * MAXSENSOR), ("sensor_objid", _i * MAXSENSOR),
         ("sensor_adr", _i * MAXSENSOR),
+        ("nmesh", _i), ("nmeshvert", _i), ("geom_dataid", _i * MAXGEOM), ("mesh_vertadr", _i * MAXMESH),
+        ("mesh_vertnum", _i * MAXMESH), ("mesh_vert", (_d * 3) * MAXMESHVERT),
     ]
+
+
+# fields a model dict may omit (images compiled before mesh support: no mesh geoms)
+_OPTIONAL_ZERO = {"nmesh", "nmeshvert", "geom_dataid", "mesh_vertadr", "mesh_vertnum", "mesh_vert"}
 
 
 def _fill(dst, val):
@@ -952,6 +1049,8 @@ def to_ctypes(m: dict) -> UR3eModelC:
     c = UR3eModelC()
     for name, _t in UR3eModelC._fields_:
         if name not in m:
+            if name in _OPTIONAL_ZERO:
+                continue
             raise KeyError(f"model dict lacks {name}")
         v = m[name]
         if isinstance(v, (list, tuple, np.ndarray)):
