@@ -31,6 +31,7 @@ def test_edited_yaml_gain_changes_ctrl_identically(tmp_path):
     ob = po.OracleBatch(ve.stepper.model_c, po.config_from(ve.stepper.cfg), n)
     ve.reset()
     vd.reset()
+    ob.reset_all()  # the Batch reset at creation and VecEnv.reset reset again: a second episode
     rng = np.random.default_rng(2)
     differs = False
     for t in range(steps):
