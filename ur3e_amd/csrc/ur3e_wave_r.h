@@ -408,40 +408,38 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
     const bool adds = lane + rb < nefc &&
                       (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC && w.jj == 0));
     unsigned long long act = __ballot(adds);
-    /* row i's operands are loaded one row ahead and pinned in registers (the asm keeps the
-       compiler from sinking the loads under the jk != 0 test, which serialised two LDS round
-       trips per element) */
-    const int ifirst = act ? (int)__builtin_ctzll(act) : 0;
-    double njk[NQ], njc[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; q++)
-      if (q < nqe) { njk[q] = s.efc_J[rb + ifirst][ek[q]]; njc[q] = s.efc_J[rb + ifirst][ec[q]]; }
-    while (act) {
-      const int i = (int)__builtin_ctzll(act);
-      act &= act - 1;
-      double jk[NQ], jc[NQ];
+    if (!act) continue;
+    /* rows in a ping-pong of two register sets: the next row's operands are loaded while this row is
+       added, then pinned (asm) after that add, so the compiler neither sinks the loads under the
+       jk != 0 test (two serial LDS round trips per element) nor copies them between iterations */
+    double ak[NQ], ac[NQ], bk[NQ], bc[NQ];
+    auto load = [&](int i, double (&jk)[NQ], double (&jc)[NQ]) {
 #pragma unroll
       for (int q = 0; q < NQ; q++)
-        if (q < nqe) {
-          jk[q] = njk[q]; jc[q] = njc[q];
-          asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
-        }
-      const int inext = act ? (int)__builtin_ctzll(act) : i;
+        if (q < nqe) { jk[q] = s.efc_J[rb + i][ek[q]]; jc[q] = s.efc_J[rb + i][ec[q]]; }
+    };
+    auto pin = [&](double (&jk)[NQ], double (&jc)[NQ]) {
 #pragma unroll
       for (int q = 0; q < NQ; q++)
-        if (q < nqe) { njk[q] = s.efc_J[rb + inext][ek[q]]; njc[q] = s.efc_J[rb + inext][ec[q]]; }
-      const int st = rli(w.st, i);
-      if (st == ST_QUADRATIC) {
+        if (q < nqe) asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
+    };
+    /* the row's increment comes from one of two branches (a quadratic row: D jk jc, skipped where
+       jk == 0; the first row of a cone-state elliptic contact, the only other kind in `act`: its
+       3x3 cone block), and hv takes it in one place after them, so the loop carries hv in the same
+       registers on both paths (updated inside the branches, hv was copied back every row) */
+    auto add = [&](int i, const double (&jk)[NQ], const double (&jc)[NQ]) {
+      double inc[NQ];
+      bool use[NQ];
+      if (rli(w.st, i) == ST_QUADRATIC) {
         const double D = rl(w.D, i);
 #pragma unroll
         for (int q = 0; q < NQ; q++)
           if (q < nqe) {
             const double djr = D * jk[q];
-            double n = hv[q] + djr * jc[q];
-            asm volatile("" : "+v"(n));
-            hv[q] = jk[q] != 0 ? n : hv[q];
+            inc[q] = djr * jc[q];
+            use[q] = jk[q] != 0;
           }
-      } else if (st == ST_CONE && rli(w.typ, i) == CN_CONTACT_ELLIPTIC && rli(w.jj, i) == 0) {
+      } else {
         const int ri = rb + i;
         const double* Hc = s.con_Hc[s.efc_id[ri]];
 #pragma unroll
@@ -455,9 +453,37 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
           }
           double acc = 0;
           for (int j = 0; j < 3; j++) acc += s.efc_J[ri + j][ec[q]] * t[j];
-          hv[q] += acc;
+          inc[q] = acc;
+          use[q] = true;
         }
       }
+#pragma unroll
+      for (int q = 0; q < NQ; q++)
+        if (q < nqe) {
+          double n = hv[q] + inc[q];
+          asm volatile("" : "+v"(n));
+          hv[q] = use[q] ? n : hv[q];
+        }
+    };
+    int i = (int)__builtin_ctzll(act);
+    act &= act - 1;
+    load(i, ak, ac);
+    pin(ak, ac);
+    while (true) {
+      const int ib = act ? (int)__builtin_ctzll(act) : i; /* the last row reloads itself (unused) */
+      load(ib, bk, bc);
+      add(i, ak, ac);
+      pin(bk, bc);
+      if (!act) break;
+      act &= act - 1;
+      i = ib;
+      const int ia = act ? (int)__builtin_ctzll(act) : i;
+      load(ia, ak, ac);
+      add(i, bk, bc);
+      pin(ak, ac);
+      if (!act) break;
+      act &= act - 1;
+      i = ia;
     }
   }
   /* element slot q of this lane is packed-triangle index ep[q] */
@@ -510,16 +536,19 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
       if (mcol) colm[lane] = h[jm < K_NV ? jm : 0];
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
+      /* every lane updates (no lane >= k select): on lanes < k the entry h[k] is the upper triangle,
+         which nothing reads (the diagonal comes from lane k, the solves and the L^T transpose read
+         c <= row only) */
 #pragma unroll
       for (int k = j + 1; k < SPLIT; k++) {
         const double lkj = col[k];
-        if (lane >= k) h[k] -= h[j] * lkj;
+        h[k] -= h[j] * lkj;
       }
       if (mcol) {
 #pragma unroll
         for (int k = jm + 1; k < NVS; k++) {
           const double lkm = colm[k];
-          if (lane >= k) h[k] -= h[jm < K_NV ? jm : 0] * lkm;
+          h[k] -= h[jm < K_NV ? jm : 0] * lkm;
         }
       }
     }
@@ -539,21 +568,23 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
         for (int k = j + 1; k < K_NV; k++) {
           if (k < nv) {
             const double lkj = col[k];
-            if (lane >= k) h[k] -= h[j] * lkj;
+            h[k] -= h[j] * lkj; /* upper-triangle entries (lane < k) are never read */
           }
         }
       }
     }
   }
   WT(12);
-  /* forward: L y = grad (x[k] = tmp[k] / L[k][k]; tmp[i] -= L[i][k] x[k], i > k) */
-  double tmp = grad;
+  /* forward: L y = grad (x[k] = tmp[k] / L[k][k]; tmp[i] -= L[i][k] x[k], i > k).  Every lane applies
+     the update (no lane > k select): lane k keeps its result in yf, and the lanes < k, already final in
+     yf, only disturb their dead tmp (their h[k] is the unread upper triangle) */
+  double tmp = grad, yf = 0.0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++) {
     if (k < nv) {
       double xk = rl(tmp, k) / rl(h[k], k);
-      if (lane == k) tmp = xk;
-      else if (lane > k) tmp -= h[k] * xk;
+      yf = lane == k ? xk : yf;
+      tmp -= h[k] * xk;
     }
   }
   WT(18);
@@ -565,21 +596,26 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  /* lt[i] = L[i][row] for i >= row; for i < row an in-range element nobody uses (KTRI(i, row) <
+     nv (nv + 1) / 2 for i < row < nv), so no select */
   double lt[K_NV];
 #pragma unroll
-  for (int i = 0; i < K_NV; i++) lt[i] = i >= row ? s.Hl[KTRI(i, row)] : 0.0;
-  /* backward: L' x = y (x[i] = tmp[i] / L[i][i]; tmp[t] -= L[i][t] x[i], t < i) */
+  for (int i = 0; i < K_NV; i++) lt[i] = s.Hl[KTRI(i, row)];
+  /* backward: L' x = y (x[i] = tmp[i] / L[i][i]; tmp[t] -= L[i][t] x[i], t < i); as the forward sweep,
+     every lane updates and lane i keeps x[i] in xf (the lanes > i are final) */
+  tmp = yf;
+  double xf = 0.0;
 #pragma unroll
   for (int i = K_NV - 1; i >= 0; i--) {
     if (i < nv) {
       double xi = rl(tmp, i) / rl(lt[i], i);
-      if (lane == i) tmp = xi;
-      else if (lane < i) tmp -= lt[i] * xi;
+      xf = lane == i ? xi : xf;
+      tmp -= lt[i] * xi;
     }
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
-  return -tmp;
+  return -xf;
 }
 
 /* line-search 1-D evaluation at a (w_ls_eval): per-row terms on the row lanes, ordered sums */
