@@ -303,6 +303,12 @@ WD void r_compute_grad(KModel m, KS& s, const RRow (&W)[KS::RPL], double Ma, dou
   grad = Ma - qs - f;
 }
 
+/* compile-time int for generic lambdas */
+template <int N>
+struct RIc {
+  static constexpr int value = N;
+};
+
 /* Newton direction: H = M + J'DJ + cone terms (lane k = row k), Cholesky in registers,
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
 template <class KS>
@@ -400,91 +406,90 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
     hv[q] = s.qMp[ep[q]];
   }
   /* only rows that add to H are visited, in row order (the others add nothing in the oracle):
-     quadratic rows and the first row of each cone-state contact; slot h covers rows 64h.. */
+     quadratic rows and the first row of each cone-state contact; slot h covers rows 64h..
+     Rows go in chunks of CH.  Every row's increment is independent of hv: D jk jc for a quadratic
+     row (-0.0 where the oracle skips jk == 0: x + (-0.0) == x for every x, signed zeros included),
+     the 3x3 cone block for the first row of a cone-state elliptic contact (the only other kind in
+     `act`).  So a chunk's loads and products overlap, and only the in-order adds hv += inc stay
+     serial: one dependent add per row and element slot.  NQE element slots are compiled in (2 in
+     the block-diagonal case, where 126 elements fill two). */
+  auto hbuild = [&](auto nqe_tag) {
+    constexpr int NQE = decltype(nqe_tag)::value;
+    constexpr int CH = NQE <= 2 ? 4 : 2;
 #pragma unroll
-  for (int h = 0; h < RPL; h++) {
-    const RRow& w = W[h];
-    const int rb = 64 * h;
-    const bool adds = lane + rb < nefc &&
-                      (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC && w.jj == 0));
-    unsigned long long act = __ballot(adds);
-    if (!act) continue;
-    /* rows in a ping-pong of two register sets: the next row's operands are loaded while this row is
-       added, then pinned (asm) after that add, so the compiler neither sinks the loads under the
-       jk != 0 test (two serial LDS round trips per element) nor copies them between iterations */
-    double ak[NQ], ac[NQ], bk[NQ], bc[NQ];
-    auto load = [&](int i, double (&jk)[NQ], double (&jc)[NQ]) {
+    for (int h = 0; h < RPL; h++) {
+      const RRow& w = W[h];
+      const int rb = 64 * h;
+      const bool adds = lane + rb < nefc &&
+                        (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC && w.jj == 0));
+      unsigned long long act = __ballot(adds);
+      while (act) {
+        int r[CH];
+        bool v[CH];
+        v[0] = true;
+        r[0] = (int)__builtin_ctzll(act);
+        act &= act - 1;
 #pragma unroll
-      for (int q = 0; q < NQ; q++)
-        if (q < nqe) { jk[q] = s.efc_J[rb + i][ek[q]]; jc[q] = s.efc_J[rb + i][ec[q]]; }
-    };
-    auto pin = [&](double (&jk)[NQ], double (&jc)[NQ]) {
-#pragma unroll
-      for (int q = 0; q < NQ; q++)
-        if (q < nqe) asm volatile("" : "+v"(jk[q]), "+v"(jc[q]));
-    };
-    /* the row's increment comes from one of two branches (a quadratic row: D jk jc, skipped where
-       jk == 0; the first row of a cone-state elliptic contact, the only other kind in `act`: its
-       3x3 cone block), and hv takes it in one place after them, so the loop carries hv in the same
-       registers on both paths (updated inside the branches, hv was copied back every row) */
-    auto add = [&](int i, const double (&jk)[NQ], const double (&jc)[NQ]) {
-      double inc[NQ];
-      bool use[NQ];
-      if (rli(w.st, i) == ST_QUADRATIC) {
-        const double D = rl(w.D, i);
-#pragma unroll
-        for (int q = 0; q < NQ; q++)
-          if (q < nqe) {
-            const double djr = D * jk[q];
-            inc[q] = djr * jc[q];
-            use[q] = jk[q] != 0;
-          }
-      } else {
-        const int ri = rb + i;
-        const double* Hc = s.con_Hc[s.efc_id[ri]];
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          if (q >= nqe) continue;
-          double t[3];
-          for (int j = 0; j < 3; j++) {
-            double acc = 0;
-            for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[ri + k][ek[q]];
-            t[j] = acc;
-          }
-          double acc = 0;
-          for (int j = 0; j < 3; j++) acc += s.efc_J[ri + j][ec[q]] * t[j];
-          inc[q] = acc;
-          use[q] = true;
+        for (int c = 1; c < CH; c++) { /* past the last row: a repeat of r[0] whose increment is -0.0 */
+          v[c] = act != 0;
+          r[c] = v[c] ? (int)__builtin_ctzll(act) : r[0];
+          act &= act - 1;
         }
+        double jk[CH][NQE], jc[CH][NQE];
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+#pragma unroll
+          for (int q = 0; q < NQE; q++)
+            if (q < nqe) { jk[c][q] = s.efc_J[rb + r[c]][ek[q]]; jc[c][q] = s.efc_J[rb + r[c]][ec[q]]; }
+        int st[CH];
+        double inc[CH][NQE];
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+          st[c] = rli(w.st, r[c]);
+          const double D = rl(w.D, r[c]);
+          const bool quad = v[c] && st[c] == ST_QUADRATIC;
+#pragma unroll
+          for (int q = 0; q < NQE; q++)
+            if (q < nqe) {
+              const double djr = D * jk[c][q];
+              double t = djr * jc[c][q];
+              t = quad && jk[c][q] != 0 ? t : -0.0;
+              asm volatile("" : "+v"(t)); /* keeps hv + t from being refolded into a select on hv */
+              inc[c][q] = t;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+          if (v[c] && st[c] != ST_QUADRATIC) {
+            const int ri = rb + r[c];
+            const double* Hc = s.con_Hc[s.efc_id[ri]];
+#pragma unroll
+            for (int q = 0; q < NQE; q++) {
+              if (q >= nqe) continue;
+              double t[3];
+              for (int j = 0; j < 3; j++) {
+                double acc = 0;
+                for (int k = 0; k < 3; k++) acc += Hc[3 * j + k] * s.efc_J[ri + k][ek[q]];
+                t[j] = acc;
+              }
+              double acc = 0;
+              for (int j = 0; j < 3; j++) acc += s.efc_J[ri + j][ec[q]] * t[j];
+              inc[c][q] = acc;
+            }
+          }
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+#pragma unroll
+          for (int q = 0; q < NQE; q++)
+            if (q < nqe) hv[q] += inc[c][q];
       }
-#pragma unroll
-      for (int q = 0; q < NQ; q++)
-        if (q < nqe) {
-          double n = hv[q] + inc[q];
-          asm volatile("" : "+v"(n));
-          hv[q] = use[q] ? n : hv[q];
-        }
-    };
-    int i = (int)__builtin_ctzll(act);
-    act &= act - 1;
-    load(i, ak, ac);
-    pin(ak, ac);
-    while (true) {
-      const int ib = act ? (int)__builtin_ctzll(act) : i; /* the last row reloads itself (unused) */
-      load(ib, bk, bc);
-      add(i, ak, ac);
-      pin(bk, bc);
-      if (!act) break;
-      act &= act - 1;
-      i = ib;
-      const int ia = act ? (int)__builtin_ctzll(act) : i;
-      load(ia, ak, ac);
-      add(i, bk, bc);
-      pin(ak, ac);
-      if (!act) break;
-      act &= act - 1;
-      i = ia;
     }
+  };
+  if constexpr (SPLIT > 0) {
+    if (bd) hbuild(RIc<2>{});
+    else hbuild(RIc<NQ>{});
+  } else {
+    hbuild(RIc<NQ>{});
   }
   /* element slot q of this lane is packed-triangle index ep[q] */
 #pragma unroll
