@@ -22,7 +22,8 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
          10: "H build", 11: "cholesky / (r) backward solve", 12: "hessian_solve / (r) cholesky",
          18: "(r) forward solve", 19: "(r) ls setup + eval(0)", 20: "(r) ls eval (per call)", 13: "line_search tail", 14: "eval+grad (iter)",
          15: "newton tail", 21: "touch sensors", 22: "badacc check", 16: "euler factor+solve", 17: "integrate", 25: "make_carry", 26: "obs+reward+termination", 27: "commit",
-         28: "(count only) block-diagonal Newton directions"}
+         28: "(count only) block-diagonal Newton directions", 29: "(r) kinematics: orientation level chain",
+         30: "(r) kinematics: position level chain", 31: "(r) com_vel: cvel level chain"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"

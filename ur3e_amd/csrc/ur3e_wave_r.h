@@ -1100,6 +1100,7 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+  WT(29);
   /* 2. orientation-only terms of every body */
   double ra[3] = {0, 0, 0}, vec[3] = {0, 0, 0};
   if (depth > 0) {
@@ -1145,6 +1146,7 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+  WT(30);
   if (lane < nfr) {
     double bp[3], bq[4], bm[9], op[3], om[9];
     for (int c = 0; c < 3; c++) bp[c] = s.xpos[fb][c];
@@ -1232,6 +1234,7 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+  WT(31);
   if (depth > 0 && one) {
     double cdd[6];
     k_cross_motion(cdd, cvp, cd);
