@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B/C...: the product library against variants built ON THE BOX from patches against HEAD
-# (tools/var/<name>.patch), so no variant library rides in the push.  Each variant first runs the fast
+# (tools/var/<name>.patch) and/or extra compiler flags (tools/var/<name>.flags), so no variant
+# library rides in the push.  Each variant first runs the fast
 # GPU parity set; then the bench alternates base and variants for ROUNDS rounds (boxes differ by ~1 %).
 # usage: tools/ab_multi.sh ROUNDS NAME...
 set -o pipefail
@@ -10,8 +11,9 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm 
 pids=""
 for v in "$@"; do
   W=/tmp/ur3e_var_$v; rm -rf $W; mkdir -p $W; cp -r $R/ur3e_amd $R/include $W/
-  (cd $W && patch -s -p1 < $R/tools/var/$v.patch) || { echo "patch $v failed"; exit 1; }
-  timeout -k 10 600 /opt/rocm/bin/hipcc $FL -o $W/lib.so $W/ur3e_amd/csrc/ur3e_batch.hip $W/ur3e_amd/csrc/ur3e_vecnorm.hip > $D/${v}_build.log 2>&1 &
+  if [ -f $R/tools/var/$v.patch ]; then (cd $W && patch -s -p1 < $R/tools/var/$v.patch) || { echo "patch $v failed"; exit 1; }; fi
+  XF=""; if [ -f $R/tools/var/$v.flags ]; then XF=$(cat $R/tools/var/$v.flags); fi
+  timeout -k 10 600 /opt/rocm/bin/hipcc $FL $XF -o $W/lib.so $W/ur3e_amd/csrc/ur3e_batch.hip $W/ur3e_amd/csrc/ur3e_vecnorm.hip > $D/${v}_build.log 2>&1 &
   pids="$pids $!"
 done
 for p in $pids; do wait $p || { echo "a variant build failed"; tail -5 $D/*_build.log; exit 1; }; done

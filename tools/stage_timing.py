@@ -23,14 +23,17 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
          18: "(r) forward solve", 19: "(r) ls setup + eval(0)", 20: "(r) ls eval (per call)", 13: "line_search tail", 14: "eval+grad (iter)",
          15: "newton tail", 21: "touch sensors", 22: "badacc check", 16: "euler factor+solve", 17: "integrate", 25: "make_carry", 26: "obs+reward+termination", 27: "commit",
          28: "(count only) block-diagonal Newton directions", 29: "(r) kinematics: orientation level chain",
-         30: "(r) kinematics: position level chain", 31: "(r) com_vel: cvel level chain"}
+         30: "(r) kinematics: position level chain", 31: "(r) com_vel: cvel level chain",
+         32: "(r) com_pos: subtree com sums", 33: "(r) com_pos: cdof", 34: "(r) crb: composite inertia sums",
+         36: "(r) constraint rows: layout", 37: "(r) constraint rows: group data", 38: "(r) constraint rows: Jacobian",
+         39: "(r) collision: broadphase", 40: "(r) tree LDL' factor (smooth + Euler)"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"
 tier = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 L = rt.load_library()
 L.ur3e_debug_stage_cycles_tier.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-cyc = (ctypes.c_ulonglong * 32)(); calls = (ctypes.c_ulonglong * 32)()
+cyc = (ctypes.c_ulonglong * 48)(); calls = (ctypes.c_ulonglong * 48)()
 if work == "gym":
     md, mc = rt.load_model("main")
     # schedule 1: the per-env-step kernel (the one with stage marks)

@@ -2315,12 +2315,12 @@ extern "C" int ur3e_debug_stage_cycles_tier(int tier, unsigned long long* cycles
 #ifdef UR3E_STAGE_TIMING
   if (tier < 0 || tier > 2) return fail(UR3E_EINVAL, "tier must be 0 (compact), 1 (grasp) or 2 (full)");
   HIPCHK(hipDeviceSynchronize());
-  unsigned long long c[3][32], k[3][32];
+  unsigned long long c[3][W_NSTAGE_MARKS], k[3][W_NSTAGE_MARKS];
   HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(ur3e_stage_cycles), sizeof(c)));
   HIPCHK(hipMemcpyFromSymbol(k, HIP_SYMBOL(ur3e_stage_calls), sizeof(k)));
-  for (int i = 0; i < 32; i++) { cycles[i] = c[tier][i]; calls[i] = k[tier][i]; }
+  for (int i = 0; i < W_NSTAGE_MARKS; i++) { cycles[i] = c[tier][i]; calls[i] = k[tier][i]; }
   if (reset) {
-    unsigned long long z[3][32] = {{0}};
+    unsigned long long z[3][W_NSTAGE_MARKS] = {{0}};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_cycles), z, sizeof(z)));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(ur3e_stage_calls), z, sizeof(z)));
   }

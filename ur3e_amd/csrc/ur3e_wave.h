@@ -34,6 +34,9 @@
 #define W_NP_STAGE 16
 
 /* host-precomputed tree bookkeeping for the cooperative stages */
+/* stage-timing marks of the -DUR3E_STAGE_TIMING build (tools/stage_timing.py) */
+#define W_NSTAGE_MARKS 48
+
 struct KPlan {
   int nlevel;
   int body_depth[K_NB];
@@ -127,8 +130,8 @@ struct KSX<MC, ME, NVC, TREE, false> {
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
   unsigned long long tlast;
 #ifdef UR3E_STAGE_TIMING
-  unsigned long long tacc[32];
-  unsigned int tcnt[32];
+  unsigned long long tacc[W_NSTAGE_MARKS];
+  unsigned int tcnt[W_NSTAGE_MARKS];
 #endif
 };
 
@@ -181,8 +184,8 @@ struct KSX<MC, ME, NVC, TREE, true> {
   int np_lanes; /* survivor lanes per narrowphase chunk (KConfig.np_lanes, <= W_NP_LANES) */
   unsigned long long tlast;
 #ifdef UR3E_STAGE_TIMING
-  unsigned int tacc[32]; /* 32-bit: keeps the timing build's layout within 20 KB (with MAXCON 9) */
-  unsigned int tcnt[32];
+  unsigned int tacc[W_NSTAGE_MARKS]; /* 32-bit: keeps the timing build's layout near 20 KB (with MAXCON 9) */
+  unsigned int tcnt[W_NSTAGE_MARKS];
 #endif
   union {
     struct {
@@ -294,8 +297,8 @@ __device__ __forceinline__ int w_any(int pred) {
 #ifdef UR3E_STAGE_TIMING
 /* [tier][stage]: tier 0 compact (KS::MAXCON <= W_SMALL_MAXCON), 1 grasp (other overlaid layouts),
    2 full capacity */
-__device__ unsigned long long ur3e_stage_cycles[3][32];
-__device__ unsigned long long ur3e_stage_calls[3][32];
+__device__ unsigned long long ur3e_stage_cycles[3][W_NSTAGE_MARKS];
+__device__ unsigned long long ur3e_stage_calls[3][W_NSTAGE_MARKS];
 #define W_TIER_OF(s)                                                                          \
   (std::remove_reference_t<decltype(s)>::MAXCON <= W_SMALL_MAXCON                           \
        ? 0                                                                                   \
@@ -317,12 +320,12 @@ __device__ unsigned long long ur3e_stage_calls[3][32];
   } while (0)
 #define WT_INIT()                                                       \
   do {                                                                  \
-    if (w_lane() < 32) { s.tacc[w_lane()] = 0; s.tcnt[w_lane()] = 0; } \
+    if (w_lane() < W_NSTAGE_MARKS) { s.tacc[w_lane()] = 0; s.tcnt[w_lane()] = 0; } \
   } while (0)
 #define WT_FLUSH()                                                      \
   do {                                                                  \
     __builtin_amdgcn_wave_barrier();                                    \
-    if (w_lane() < 32 && s.tcnt[w_lane()]) {                      \
+    if (w_lane() < W_NSTAGE_MARKS && s.tcnt[w_lane()]) {          \
       atomicAdd(&ur3e_stage_cycles[W_TIER_OF(s)][w_lane()], (unsigned long long)s.tacc[w_lane()]);  \
       atomicAdd(&ur3e_stage_calls[W_TIER_OF(s)][w_lane()], (unsigned long long)s.tcnt[w_lane()]); \
     }                                                                   \
@@ -449,6 +452,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
       }
     }
     SYNC();
+    WT(32);
   } else {
     if (tid < nb) {
       int i = tid;
@@ -496,6 +500,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
       s.cdof[da][3] = cr[0]; s.cdof[da][4] = cr[1]; s.cdof[da][5] = cr[2];
     }
   }
+  WT(33);
   if constexpr (KS::OVERLAY) {
     /* connect anchors for the constraint rows (r_mc_rows), while xmat is still alive */
     for (int e = tid; e < m->neq; e += NT) {
@@ -571,6 +576,7 @@ WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
     r_subtree_sum<10, true>(m, crb);
     if (tid < nb)
       for (int k = 0; k < 10; k++) s.u.body.b10[tid][k] = crb[k];
+    WT(34);
   } else {
     for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
   }
@@ -844,6 +850,7 @@ WD void r_collision(KModel m, KS& s) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  WT(39);
   int total = 0;
   if constexpr (KS::OVERLAY) {
     /* survivors in chunks of W_NP_LANES lanes: narrowphase with its clip polygons in LDS, raw
@@ -1017,6 +1024,7 @@ WD void w_make_constraint(KModel m, const KPlan* __restrict__ pl, KS& s) {
   constexpr bool REG = (NT == 64 && KS::OVERLAY);
   if constexpr (REG) {
     r_mc_layout(m, pl, s);
+    WT(36);
     if (s.ovf) return;
       r_mc_rows(m, pl, s);
   } else {

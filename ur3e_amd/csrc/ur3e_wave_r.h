@@ -954,6 +954,7 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
       }
     }
   }
+  WT(40);
   double dg = 1.0;
 #pragma unroll
   for (int i = 0; i < K_NV; i++)
@@ -1452,61 +1453,68 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
       for (int k = 0; k < 5; k++) simp[k] = m->cpair_solimp[p][k];
     }
   }
-  /* ---- 2. Jacobian, lane = dof, groups in order ---- */
+  WT(37);
+  /* ---- 2. Jacobian: GS groups side by side per pass (lanes [K_NV t, K_NV t + K_NV) take group
+     g0 + t, lane = dof within), the group's data by lane shuffle from its group lane, gathered
+     with the whole wave active (no permute under divergent control flow) ---- */
   {
-    const int v = lane < nv ? lane : 0;
+    constexpr int GS = 64 / K_NV;
+    const int slot = lane / K_NV;
+    const int v = lane - slot * K_NV;
+    const int vv = v < nv ? v : 0;
     double cd[6];
-    for (int r = 0; r < 6; r++) cd[r] = s.cdof[v][r];
-    const unsigned int vbit = 1u << v;
-    for (int g = 0; g < ngrp; g++) {
-      const int type = rli(gtype, g), r = rli(grow, g);
-      if (type == G_CONNECT || type >= G_CONTACT) {
-        const unsigned int m1 = (unsigned int)rli(msk1, g), m2 = (unsigned int)rli(msk2, g);
-        double a1[3], a2[3], j1[3], j2[3];
-        for (int k = 0; k < 3; k++) { a1[k] = rl(o1[k], g); a2[k] = rl(o2[k], g); }
-        if (m1 & vbit) {
-          double cr[3];
-          k_cross3(cr, cd, a1);
-          j1[0] = cd[3] + cr[0]; j1[1] = cd[4] + cr[1]; j1[2] = cd[5] + cr[2];
-        } else {
-          j1[0] = 0; j1[1] = 0; j1[2] = 0;
-        }
-        if (m2 & vbit) {
-          double cr[3];
-          k_cross3(cr, cd, a2);
-          j2[0] = cd[3] + cr[0]; j2[1] = cd[4] + cr[1]; j2[2] = cd[5] + cr[2];
-        } else {
-          j2[0] = 0; j2[1] = 0; j2[2] = 0;
-        }
-        if (type == G_CONNECT) {
-          if (lane < nv)
+    for (int r = 0; r < 6; r++) cd[r] = s.cdof[vv][r];
+    const unsigned int vbit = 1u << vv;
+    for (int g0 = 0; g0 < ngrp; g0 += GS) {
+      const int g = g0 + slot;
+      const bool on = slot < GS && g < ngrp && v < nv;
+      const int gs = on ? g : 0;
+      const int type = shfi(gtype, gs), r = shfi(grow, gs);
+      const unsigned int m1 = (unsigned int)shfi(msk1, gs), m2 = (unsigned int)shfi(msk2, gs);
+      const int d1 = shfi(dof1, gs), d2 = shfi(dof2, gs);
+      double a1[3], a2[3], f[9];
+      for (int k = 0; k < 3; k++) { a1[k] = shf(o1[k], gs); a2[k] = shf(o2[k], gs); }
+      for (int k = 0; k < 9; k++) f[k] = shf(fr[k], gs);
+      const double dp = shf(dpoly, gs), sd = shf(side, gs);
+      if (on) {
+        if (type == G_CONNECT || type >= G_CONTACT) {
+          double j1[3], j2[3];
+          if (m1 & vbit) {
+            double cr[3];
+            k_cross3(cr, cd, a1);
+            j1[0] = cd[3] + cr[0]; j1[1] = cd[4] + cr[1]; j1[2] = cd[5] + cr[2];
+          } else {
+            j1[0] = 0; j1[1] = 0; j1[2] = 0;
+          }
+          if (m2 & vbit) {
+            double cr[3];
+            k_cross3(cr, cd, a2);
+            j2[0] = cd[3] + cr[0]; j2[1] = cd[4] + cr[1]; j2[2] = cd[5] + cr[2];
+          } else {
+            j2[0] = 0; j2[1] = 0; j2[2] = 0;
+          }
+          if (type == G_CONNECT) {
             for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = j1[k] - j2[k];
-        } else {
-          double f[9];
-          for (int k = 0; k < 9; k++) f[k] = rl(fr[k], g);
-          const double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
-          if (lane < nv)
+          } else {
+            const double dj0 = j2[0] - j1[0], dj1 = j2[1] - j1[1], dj2 = j2[2] - j1[2];
             for (int k = 0; k < 3; k++) s.efc_J[r + k][v] = f[3 * k] * dj0 + f[3 * k + 1] * dj1 + f[3 * k + 2] * dj2;
+          }
+        } else if (type == G_JOINTEQ) {
+          double val = 0;
+          if (v == d1) val = 1;
+          if (d2 >= 0 && v == d2) val = -dp;
+          s.efc_J[r][v] = val;
+        } else if (type == G_FLOSS) {
+          s.efc_J[r][v] = v == d1 ? 1.0 : 0.0;
+        } else {
+          s.efc_J[r][v] = v == d1 ? -sd : 0.0;
         }
-      } else if (type == G_JOINTEQ) {
-        const int d1 = rli(dof1, g), d2 = rli(dof2, g);
-        const double dp = rl(dpoly, g);
-        double val = 0;
-        if (v == d1) val = 1;
-        if (d2 >= 0 && v == d2) val = -dp;
-        if (lane < nv) s.efc_J[r][v] = val;
-      } else if (type == G_FLOSS) {
-        const int d1 = rli(dof1, g);
-        if (lane < nv) s.efc_J[r][v] = v == d1 ? 1.0 : 0.0;
-      } else {
-        const int d1 = rli(dof1, g);
-        const double sd = rl(side, g);
-        if (lane < nv) s.efc_J[r][v] = v == d1 ? -sd : 0.0;
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  WT(38);
   /* ---- 3. impedance, lane = row (w_row_impedance); row lane + 64 h for each row slot ---- */
   constexpr int SPLIT = KS::STATIC_TREE ? UR3E_MAIN_SPLIT : 0;
   int couples = 0; /* a row of this lane has nonzeros in both dof trees */
