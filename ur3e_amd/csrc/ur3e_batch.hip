@@ -1751,6 +1751,14 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     for (int j = dof; j >= 0; j = m->dof_parentid[j]) mask |= 1u << j;
     pl->body_dof_mask[b] = mask;
   }
+  for (int b = 0; b < m->nbody; b++) {
+    const int jfc = m->body_jntnum[b] ? m->body_jntadr[b] : 0;
+    pl->bj_type[b] = m->jnt_type[jfc];
+    pl->bj_qadr[b] = m->jnt_qposadr[jfc];
+    pl->bj_q0[b] = m->qpos0[pl->bj_qadr[b]];
+    for (int c = 0; c < 3; c++) { pl->bj_axis[b][c] = m->jnt_axis[jfc][c]; pl->bj_pos[b][c] = m->jnt_pos[jfc][c]; }
+  }
+  for (int j = 0; j < m->njnt; j++) pl->jnt_root[j] = m->body_rootid[m->jnt_bodyid[j]];
   for (int v = 0; v < m->nv; v++)
     if (m->dof_frictionloss[v] > 0) pl->floss_dof[pl->nfloss++] = v;
   for (int b = 0; b < m->nbody; b++)

@@ -55,6 +55,12 @@ struct KPlan {
      each dof of a fixed tendon, 0 elsewhere); model constants, so computed once on the host */
   double act_moment[K_NU][K_NV];
   int ten_qadr[UR3E_MAXTEN][UR3E_MAXTENWRAP]; /* qpos address of each fixed-tendon dof */
+  /* per body, its first joint's constants (joint 0's for a body without joints, as the passes
+     index it), and per joint its body's root: the compact tier's body passes then load every model
+     constant one level deep instead of through body -> joint -> qpos index chains */
+  int bj_type[K_NB], bj_qadr[K_NB];
+  double bj_q0[K_NB], bj_axis[K_NB][3], bj_pos[K_NB][3];
+  int jnt_root[K_NJ];
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -479,7 +485,7 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
   for (int j = tid; j < m->njnt; j += NT) {
     int b = m->jnt_bodyid[j];
     int da = m->jnt_dofadr[j];
-    const double* c = s.subtree_com[m->body_rootid[b]];
+    const double* c = s.subtree_com[pl->jnt_root[j]];
     double off[3] = {c[0] - s.xanchor[j][0], c[1] - s.xanchor[j][1], c[2] - s.xanchor[j][2]};
     if (m->jnt_type[j] == UR3E_JNT_FREE) {
       for (int k = 0; k < 3; k++) {

@@ -1040,13 +1040,13 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int pid = m->body_parentid[b];
   const int jn = m->body_jntnum[b];
   const int jf = m->body_jntadr[b];
-  const int jfc = jn ? jf : 0;
-  const int jt = m->jnt_type[jfc];
-  const int qa = m->jnt_qposadr[jfc];
+  /* the body's joint constants flattened per body in the plan: one load level */
+  const int jt = pl->bj_type[b];
+  const int qa = pl->bj_qadr[b];
   double bpos[3], bquat[4], jax[3], jps[3];
-  for (int c = 0; c < 3; c++) { bpos[c] = m->body_pos[b][c]; jax[c] = m->jnt_axis[jfc][c]; jps[c] = m->jnt_pos[jfc][c]; }
+  for (int c = 0; c < 3; c++) { bpos[c] = m->body_pos[b][c]; jax[c] = pl->bj_axis[b][c]; jps[c] = pl->bj_pos[b][c]; }
   for (int c = 0; c < 4; c++) bquat[c] = m->body_quat[b][c];
-  const double q0 = m->qpos0[qa];
+  const double q0 = pl->bj_q0[b];
   /* frames hanging off bodies: lane g < ngeom -> geom g, then sites */
   const int ng = m->ngeom, nfr = m->ngeom + m->nsite;
   int fb = 0;
@@ -1177,7 +1177,9 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int pid = m->body_parentid[b];
   const int bda = m->body_dofadr[b];
   const int bdn = m->body_dofnum[b];
-  const int jt = bdn ? m->jnt_type[m->dof_jntid[bda]] : UR3E_JNT_HINGE;
+  /* one joint per body on this path's models: the first dof's joint is the body's first joint */
+  const bool onejnt = KS::STATIC_TREE || pl->max_jntnum <= 1;
+  const int jt = bdn ? (onejnt ? pl->bj_type[b] : m->jnt_type[m->dof_jntid[bda]]) : UR3E_JNT_HINGE;
   double (*cacc)[10] = s.u.body.b10;
   /* single-dof bodies: their cdof row and qvel, loaded up front */
   double cd[6] = {0, 0, 0, 0, 0, 0}, qv = 0;
@@ -1208,7 +1210,7 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
         /* general body (free joint, several dofs, none): w_com_vel, and its cacc term */
         for (int j = 0; j < bdn; j++) {
           int dof = bda + j;
-          int jtj = m->jnt_type[m->dof_jntid[dof]];
+          int jtj = onejnt ? jt : m->jnt_type[m->dof_jntid[dof]];
           if (jtj == UR3E_JNT_FREE) {
             for (int k = 0; k < 3; k++)
               for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
