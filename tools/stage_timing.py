@@ -26,7 +26,9 @@ names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep 
          30: "(r) kinematics: position level chain", 31: "(r) com_vel: cvel level chain",
          32: "(r) com_pos: subtree com sums", 33: "(r) com_pos: cdof", 34: "(r) crb: composite inertia sums",
          36: "(r) constraint rows: layout", 37: "(r) constraint rows: group data", 38: "(r) constraint rows: Jacobian",
-         39: "(r) collision: broadphase", 40: "(r) tree LDL' factor (smooth + Euler)"}
+         39: "(r) collision: broadphase", 40: "(r) tree LDL' factor (smooth + Euler)",
+         41: "(r) eval: J.qacc, M.qacc", 42: "(r) eval: constraint update", 43: "(r) eval: cost sums",
+         44: "(r) grad: J'f", 45: "(r) ls eval: row terms", 46: "(r) ls eval: sums", 47: "(r) direction: cone Hessians"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"

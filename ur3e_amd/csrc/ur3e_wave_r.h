@@ -252,7 +252,9 @@ WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs
   }
 #pragma unroll
   for (int h = 0; h < RPL; h++) W[h].jar = r_row_dot(s, nv, nefc, qv, lane + 64 * h) - W[h].aref;
+  WT(41);
   r_constraint_update(W);
+  WT(42);
   double term = (Ma - qs) * (qacc - qas);
   /* skipped rows contribute -0.0: x + (-0.0) == x exactly for every x (incl. -0, inf, NaN), so
      the ordered sum needs neither a branch nor a select per row */
@@ -278,6 +280,7 @@ WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs
   const double a0 = rl(acc, 0), a1 = rl(acc, 1);
   gauss = 0.5 * a0;
   cost = gauss + a1;
+  WT(43);
 }
 
 /* w_compute_grad: lane k: qfrc_constraint[k] = sum_i J[i][k] force[i] (row order), grad */
@@ -301,6 +304,7 @@ WD void r_compute_grad(KModel m, KS& s, const RRow (&W)[KS::RPL], double Ma, dou
   r_slot_done();
   qfrc_c = f;
   grad = Ma - qs - f;
+  WT(44);
 }
 
 /* compile-time int for generic lambdas */
@@ -356,6 +360,7 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  WT(47);
   const int row = lane < nv ? lane : 0;
   /* H = M + J'DJ + cone blocks in ELEMENT layout: lane owns lower-triangle elements
      e = lane + 64 q (q < 4), each accumulating rows in oracle order; then one LDS transpose
@@ -720,6 +725,7 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
     /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
     Fm[h] = flag ? F : -0.0; dFm[h] = flag ? dF : -0.0; d2Fm[h] = flag == 1 ? d2F : -0.0;
   }
+  WT(45);
   double aF = gauss + a * g1 + 0.5 * a * a * g2;
   double adF = g1 + a * g2;
   double ad2F = g2;
@@ -740,6 +746,7 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
   for (int i = 0; i < nefc; i++) acc += bs[i];
   r_slot_done();
   lsF = rl(acc, 0); lsdF = rl(acc, 1); lsd2F = rl(acc, 2);
+  WT(46);
 }
 
 /* w_line_search: returns alpha (uniform); Jv on the row lanes */
