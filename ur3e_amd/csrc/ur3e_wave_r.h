@@ -126,6 +126,8 @@ WD void r_constraint_update(RRow (&W)[RPL]) {
     f2v[h] = Dm * NT_ * mu * U2 / T * w.fr1;
     zv[h] = z;
   }
+  /* one code path for every row kind (selects, no per-kind branches): the quadratic terms are formed
+     once with the expressions every kind used, the linear friction and cone values beside them */
 #pragma unroll
   for (int h = 0; h < RPL; h++) {
     RRow& w = W[h];
@@ -133,51 +135,23 @@ WD void r_constraint_update(RRow (&W)[RPL]) {
     int zs = shfri(zv, w.first);
     double f1s = shfr(f1v, w.first), f2s = shfr(f2v, w.first);
     const int t = w.typ;
-    if (t == CN_EQUALITY) {
-      w.force = -D * jar;
-      w.F = 0.5 * D * jar * jar; w.flag = 1;
-      w.st = ST_QUADRATIC;
-    } else if (t == CN_FRICTION_DOF) {
-      double fl = w.floss;
-      if (jar <= -R * fl) {
-        w.force = fl;
-        w.F = -0.5 * R * fl * fl - fl * jar;
-        w.st = ST_LINEARNEG;
-      } else if (jar >= R * fl) {
-        w.force = -fl;
-        w.F = -0.5 * R * fl * fl + fl * jar;
-        w.st = ST_LINEARPOS;
-      } else {
-        w.force = -D * jar;
-        w.F = 0.5 * D * jar * jar;
-        w.st = ST_QUADRATIC;
-      }
-      w.flag = 1;
-    } else if (t == CN_LIMIT_JOINT) {
-      if (jar >= 0) {
-        w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
-      } else {
-        w.force = -D * jar;
-        w.F = 0.5 * D * jar * jar; w.flag = 1;
-        w.st = ST_QUADRATIC;
-      }
-    } else if (t >= 0) {
-      if (zs == 0) {
-        w.force = 0; w.st = ST_SATISFIED; w.flag = 0;
-      } else if (zs == 1) {
-        w.force = -D * jar;
-        w.F = 0.5 * D * jar * jar;
-        w.flag = 1;
-        w.st = ST_QUADRATIC;
-      } else {
-        w.st = ST_CONE;
-        if (w.jj == 0) { w.F = Fmv[h]; w.flag = 1; w.force = f0v[h]; }
-        else if (w.jj == 1) { w.flag = 0; w.force = f1s; }
-        else { w.flag = 0; w.force = f2s; }
-      }
-    } else {
-      w.flag = 0; w.force = 0; w.st = ST_SATISFIED;
-    }
+    const bool fric = t == CN_FRICTION_DOF;
+    const bool contact = t >= 0 && t != CN_EQUALITY && !fric && t != CN_LIMIT_JOINT;
+    const double fl = w.floss;
+    const bool lneg = fric && jar <= -R * fl;
+    const bool lpos = fric && !lneg && jar >= R * fl;
+    const bool quad = t == CN_EQUALITY || (fric && !lneg && !lpos) || (t == CN_LIMIT_JOINT && !(jar >= 0)) ||
+                      (contact && zs == 1);
+    const bool cone = contact && zs != 0 && zs != 1;
+    const double qforce = -D * jar, qF = 0.5 * D * jar * jar;
+    const double lF0 = -0.5 * R * fl * fl;
+    const double lFn = lF0 - fl * jar, lFp = lF0 + fl * jar;
+    const int jj = w.jj;
+    const double cforce = jj == 0 ? f0v[h] : (jj == 1 ? f1s : f2s);
+    w.force = quad ? qforce : (lneg ? fl : (lpos ? -fl : (cone ? cforce : 0.0)));
+    w.F = quad ? qF : (lneg ? lFn : (lpos ? lFp : (cone && jj == 0 ? Fmv[h] : w.F)));
+    w.flag = (quad || lneg || lpos || (cone && jj == 0)) ? 1 : 0;
+    w.st = quad ? ST_QUADRATIC : (lneg ? ST_LINEARNEG : (lpos ? ST_LINEARPOS : (cone ? ST_CONE : ST_SATISFIED)));
   }
 }
 
@@ -703,25 +677,22 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
     double x = w.jar + a * w.Jv;
     double v = w.Jv;
     int zs = shfri(zv, w.first);
-    double F = 0, dF = 0, d2F = 0;
-    int flag = 0;
+    /* one code path for every row kind, as in r_constraint_update */
     const int t = w.typ;
-    if (t == CN_EQUALITY) {
-      F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
-    } else if (t == CN_FRICTION_DOF) {
-      double fl = w.floss;
-      if (x <= -R * fl) { F = -0.5 * R * fl * fl - fl * x; dF = -fl * v; flag = 2; }
-      else if (x >= R * fl) { F = -0.5 * R * fl * fl + fl * x; dF = fl * v; flag = 2; }
-      else { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
-    } else if (t == CN_LIMIT_JOINT) {
-      if (x < 0) { F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1; }
-    } else if (t >= 0) {
-      if (zs == 1) {
-        F = 0.5 * D * x * x; dF = D * x * v; d2F = D * v * v; flag = 1;
-      } else if (zs == 2 && w.jj == 0) {
-        F = cFv[h]; dF = cdFv[h]; d2F = cd2Fv[h]; flag = 1;
-      }
-    }
+    const bool fric = t == CN_FRICTION_DOF;
+    const bool contact = t >= 0 && t != CN_EQUALITY && !fric && t != CN_LIMIT_JOINT;
+    const double fl = w.floss;
+    const bool lneg = fric && x <= -R * fl;
+    const bool lpos = fric && !lneg && x >= R * fl;
+    const bool quad = t == CN_EQUALITY || (fric && !lneg && !lpos) || (t == CN_LIMIT_JOINT && x < 0) ||
+                      (contact && zs == 1);
+    const bool cone = contact && zs == 2 && w.jj == 0;
+    const double qF = 0.5 * D * x * x, qdF = D * x * v, qd2F = D * v * v;
+    const double lF0 = -0.5 * R * fl * fl;
+    const double F = quad ? qF : (lneg ? lF0 - fl * x : (lpos ? lF0 + fl * x : cFv[h]));
+    const double dF = quad ? qdF : (lneg ? -fl * v : (lpos ? fl * v : cdFv[h]));
+    const double d2F = quad ? qd2F : cd2Fv[h];
+    const int flag = (quad || cone) ? 1 : ((lneg || lpos) ? 2 : 0);
     /* skipped terms are -0.0 (exact identity for +), see r_eval_state */
     Fm[h] = flag ? F : -0.0; dFm[h] = flag ? dF : -0.0; d2Fm[h] = flag == 1 ? d2F : -0.0;
   }
