@@ -199,6 +199,34 @@ WD void r_stage_rows(double* slot, const double (&v)[RPL]) {
   asm volatile("" ::: "memory");
 }
 
+/* ordered sum acc + sl[0] + ... + sl[n-1] over an LDS slot whose entries past n are -0.0 (the exact
+   additive identity), so the count rounds up to a multiple of 8 (<= the slot's 64 * RPL entries):
+   chunks of 8 reads, the next chunk's reads issued before the current chunk's dependent adds */
+WD double r_osum(const double* sl, int n, double acc) {
+  const int n8 = (n + 7) & ~7;
+  double a[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) a[k] = sl[k];
+  for (int i = 0; i < n8;) {
+    if (i + 8 < n8) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) b[k] = sl[i + 8 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc += a[k];
+    i += 8;
+    if (i >= n8) break;
+    if (i + 8 < n8) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) a[k] = sl[i + 8 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc += b[k];
+    i += 8;
+  }
+  return acc;
+}
+
 /* uniform copy of a dof vector held one element per lane */
 WD void r_bcast(double v, int nv, double out[K_NV]) {
 #pragma unroll
@@ -247,9 +275,7 @@ WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs
      max(nv, nefc) entries: the tails are -0.0, so each equals its own ordered sum */
   const int nsum = nv > nefc ? nv : nefc;
   const double* ss = lane == 1 ? sf : st;
-  double acc = 0;
-#pragma unroll 4
-  for (int i = 0; i < nsum; i++) acc += ss[i];
+  const double acc = r_osum(ss, nsum, 0.0);
   r_slot_done();
   const double a0 = rl(acc, 0), a1 = rl(acc, 1);
   gauss = 0.5 * a0;
@@ -273,8 +299,33 @@ WD void r_compute_grad(KModel m, KS& s, const RRow (&W)[KS::RPL], double Ma, dou
 #pragma unroll
   for (int h = 0; h < RPL; h++) fv[h] = W[h].force;
   r_stage_rows(fs, fv);
+  /* full chunks of 8 rows with the next chunk's J and force reads issued before the current chunk's
+     dependent adds, then the remaining rows (row order throughout) */
+  const int nfull = nefc & ~7;
+  if (nfull > 0) {
+    double ja[8], fa[8], jb[8], fb[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { ja[k] = s.efc_J[k][col]; fa[k] = fs[k]; }
+    for (int i = 0; i < nfull;) {
+      if (i + 8 < nfull) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) { jb[k] = s.efc_J[i + 8 + k][col]; fb[k] = fs[i + 8 + k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) f = f + ja[k] * fa[k];
+      i += 8;
+      if (i >= nfull) break;
+      if (i + 8 < nfull) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) { ja[k] = s.efc_J[i + 8 + k][col]; fa[k] = fs[i + 8 + k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) f = f + jb[k] * fb[k];
+      i += 8;
+    }
+  }
 #pragma unroll 4
-  for (int i = 0; i < nefc; i++) f = f + s.efc_J[i][col] * fs[i];
+  for (int i = nfull; i < nefc; i++) f = f + s.efc_J[i][col] * fs[i];
   r_slot_done();
   qfrc_c = f;
   grad = Ma - qs - f;
@@ -712,9 +763,7 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
      one LDS read and one add per row instead of three, same operands in the same order */
   const int sel = lane == 1 ? 1 : (lane == 2 ? 2 : 0);
   const double* bs = R_SLOT(s, sel);
-  double acc = sel == 0 ? aF : (sel == 1 ? adF : ad2F);
-#pragma unroll 4
-  for (int i = 0; i < nefc; i++) acc += bs[i];
+  const double acc = r_osum(bs, nefc, sel == 0 ? aF : (sel == 1 ? adF : ad2F));
   r_slot_done();
   lsF = rl(acc, 0); lsdF = rl(acc, 1); lsd2F = rl(acc, 2);
   WT(46);
