@@ -17,7 +17,7 @@ if not os.path.exists(LIB):
 os.environ["UR3E_LIB"] = LIB
 import torch
 from ur3e_amd import runtime as rt
-names = {24: "load state+action+carry", 23: "controller / step_pre / reset prep (before each forward)", 0: "kinematics", 1: "com_pos", 2: "crb+copy", 3: "factor_tree(M)", 4: "collision", 5: "make_constraint",
+names = {24: "load state+action+carry", 35: "controller (lane 0, substep 0)", 23: "step_pre / reset prep (before each forward)", 0: "kinematics", 1: "com_pos", 2: "crb+copy", 3: "factor_tree(M)", 4: "collision", 5: "make_constraint",
          6: "com_vel", 7: "rne+passive+act", 8: "solve_tree(smooth)", 9: "newton init (eval x2-3, grad)",
          10: "H build", 11: "cholesky / (r) backward solve", 12: "hessian_solve / (r) cholesky",
          18: "(r) forward solve", 19: "(r) ls setup + eval(0)", 20: "(r) ls eval (per call)", 13: "line_search tail", 14: "eval+grad (iter)",

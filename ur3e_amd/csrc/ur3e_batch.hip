@@ -652,9 +652,10 @@ KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
   res[3] = cv[3] - cr[0]; res[4] = cv[4] - cr[1]; res[5] = cv[5] - cr[2];
 }
 
-/* UR3eEnv2._get_obs (ur3e_env2.py:111-123), lane 0 */
+/* UR3eEnv2._get_obs (ur3e_env2.py:111-123), lane 0.  pads >= 0: the pad-contact scan below done
+   beforehand by w_contact_flags (bit 0 left pad, bit 1 right pad) */
 template <class KS>
-KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
+KD void w_obs_v2(KModel m, const KS& s, double obs[24], int pads = -1) {
   int st = m->id_site_tcp, sh = m->id_site_handle, gb = m->id_body_ghost;
   const double* tcp = s.site_xpos[st];
   const double* mug = s.site_xpos[sh];
@@ -679,11 +680,16 @@ KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
   obs[21] = s.qpos[6];
   obs[22] = s.qvel[6];
   int lp = 0, rp = 0;
-  for (int ci = 0; ci < s.ncon; ci++) {
-    int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
-    if (!(b1 == m->id_body_fish || b2 == m->id_body_fish)) continue;
-    if (b1 == m->id_body_lpad || b2 == m->id_body_lpad) lp = 1;
-    if (b1 == m->id_body_rpad || b2 == m->id_body_rpad) rp = 1;
+  if (pads >= 0) {
+    lp = pads & 1;
+    rp = (pads >> 1) & 1;
+  } else {
+    for (int ci = 0; ci < s.ncon; ci++) {
+      int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+      if (!(b1 == m->id_body_fish || b2 == m->id_body_fish)) continue;
+      if (b1 == m->id_body_lpad || b2 == m->id_body_lpad) lp = 1;
+      if (b1 == m->id_body_rpad || b2 == m->id_body_rpad) rp = 1;
+    }
   }
   int robust = 0;
   if (lp + rp == 2) {
@@ -693,10 +699,12 @@ KD void w_obs_v2(KModel m, const KS& s, double obs[24]) {
   obs[23] = (double)robust;
 }
 
+/* armc >= 0: the arm self-contact scan below done beforehand by w_contact_flags (bit 2) */
 template <class KS>
-KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
+KD int w_termination_v2(KModel m, const KS& s, const double obs[24], int armc = -1) {
   double dx = obs[0] - obs[3], dy = obs[1] - obs[4], dz = obs[2] - obs[5];
   if (1.0 < sqrt(dx * dx + dy * dy + dz * dz)) return 1;
+  if (armc >= 0) return (armc >> 2) & 1 ? 1 : obs[5] <= m->fish_topple_z;
   for (int ci = 0; ci < s.ncon; ci++) {
     int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
     int a1 = (m->mask_arm_bodies >> b1) & 1, a2 = (m->mask_arm_bodies >> b2) & 1;
@@ -708,6 +716,26 @@ KD int w_termination_v2(KModel m, const KS& s, const double obs[24]) {
   }
   if (obs[5] <= m->fish_topple_z) return 1;
   return 0;
+}
+
+/* the contact-list scans of w_obs_v2 (gripper pads on the mug) and w_termination_v2 (arm self-contact)
+   with one contact per lane: each scan is an OR over the list, so the order does not matter, and the
+   per-contact body-id loads are issued together instead of one dependent pair per contact on lane 0.
+   bit 0: fish-left pad, bit 1: fish-right pad, bit 2: arm-arm contact that is not gripper-gripper.
+   Uniform result. */
+template <int NT, class KS>
+WD int w_contact_flags(KModel m, const KS& s) {
+  int lp = 0, rp = 0, arm = 0;
+  for (int ci = w_lane(); ci < s.ncon; ci += NT) {
+    const int b1 = m->geom_bodyid[s.con_geom1[ci]], b2 = m->geom_bodyid[s.con_geom2[ci]];
+    const bool fish = b1 == m->id_body_fish || b2 == m->id_body_fish;
+    lp |= fish && (b1 == m->id_body_lpad || b2 == m->id_body_lpad);
+    rp |= fish && (b1 == m->id_body_rpad || b2 == m->id_body_rpad);
+    const int a1 = (m->mask_arm_bodies >> b1) & 1, a2 = (m->mask_arm_bodies >> b2) & 1;
+    const int g1 = (m->mask_gripper_bodies >> b1) & 1, g2 = (m->mask_gripper_bodies >> b2) & 1;
+    arm |= a1 && a2 && !(g1 && g2);
+  }
+  return w_any<NT>(lp) | (w_any<NT>(rp) << 1) | (w_any<NT>(arm) << 2);
 }
 
 /* gym_utils.get_self_collision / get_table_collision (gym_utils.py:146-197) on the LDS contact list */
@@ -1095,6 +1123,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       if (k < m->nu) s.ctrl[k] = ctrl[k];
   }
   SYNC();
+  WT(35);
   const int fs = (k_is_gym(TASK) || TASK == UR3E_TASK_CTRL) ? c.frame_skip : 1;
   /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
   int sub = sub_begin, retried = 0, resetting = 0;
@@ -1163,12 +1192,14 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       o.r = r;
       o.term = term;
       o.trunc = trunc;
-    } else if (tid == 0) {
+    }
+    const int cfl = TASK == UR3E_TASK_GYM_V2 ? w_contact_flags<NT>(m, s) : 0;
+    if (tid == 0 && TASK == UR3E_TASK_GYM_V2) {
       int t = o.t + 1;
       o.t = t;
-      w_obs_v2(m, s, o.obs);
+      w_obs_v2(m, s, o.obs, cfl);
       double r = k_reward_v2(o.obs, o.a);
-      int term = w_termination_v2(m, s, o.obs);
+      int term = w_termination_v2(m, s, o.obs, cfl);
       int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
       double dx = o.obs[3] - o.obs[6], dy = o.obs[4] - o.obs[7], dz = o.obs[5] - o.obs[8];
       if (sqrt(dx * dx + dy * dy + dz * dz) < 0.05) {
