@@ -958,26 +958,73 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
       if (lane == i && i < nv) a[i] += add;
   }
   const unsigned int lbit = lane < 32 ? (1u << lane) : 0u;
+  /* main.xml: the dofs split into two trees [0, S) and [S, nv) with no ancestor across (the arm with
+     the gripper, the mug's free joint), so no element of one tree is ever updated by a pivot of the
+     other.  Their pivots are paired, S - 1 - t with nv - 1 - t in step t: one division, one staged
+     multiplier slot (lanes [0, S) carry the first tree's, lanes [S, nv) the second's) and both
+     update sets per step, so the two pivot chains overlap.  Every element still gets its updates in
+     the oracle's (descending pivot) order: bit-identical. */
+  constexpr int SPLIT = KS::STATIC_TREE ? UR3E_MAIN_SPLIT : 0;
+  if constexpr (SPLIT > 0) {
+    constexpr int NVS = KS::NV;
+    static_assert(NVS - SPLIT <= SPLIT, "paired tree LDL': trailing dof tree larger than the leading one");
+    const bool lb = lane >= SPLIT;
 #pragma unroll
-  for (int k = K_NV - 1; k >= 0; k--) {
-    if (k < nv) {
-      double akk = rl(a[k], k);
-      if (akk < K_MINVAL) akk = K_MINVAL;
-      if (lane == k) a[k] = akk;
-      const unsigned int am = amask[k];
-      if (am) {
-        double tmp = a[k] / akk; /* lane i in anc(k): A[k][i] / A[k][k] */
-        /* the multipliers reach every lane through an LDS slot (broadcast reads) */
-        double* tk = R_SLOT(s, k & 1);
+    for (int t = 0; t < SPLIT; t++) {
+      const int ka = SPLIT - 1 - t, km0 = NVS - 1 - t;
+      const bool mcol = km0 >= SPLIT; /* compile-time (t unrolled) */
+      const int km = mcol ? km0 : 0;
+      double akka = rl(a[ka], ka);
+      if (akka < K_MINVAL) akka = K_MINVAL;
+      double akkm = mcol ? rl(a[km], km) : 1.0;
+      if (akkm < K_MINVAL) akkm = K_MINVAL;
+      if (lane == ka) a[ka] = akka;
+      if (mcol && lane == km) a[km] = akkm;
+      const unsigned int ama = amask[ka], amm = mcol ? amask[km] : 0u;
+      if (ama | amm) {
+        const double tmp = (lb ? a[km] : a[ka]) / (lb ? akkm : akka);
+        double* tk = R_SLOT(s, t & 1);
         r_stage(tk, tmp);
 #pragma unroll
-        for (int i = 0; i < k; i++) {
-          if ((am >> i) & 1u) {
+        for (int i = 0; i < ka; i++) {
+          if ((ama >> i) & 1u) {
             const double ti = tk[i];
-            if ((am & lbit) && lane <= i) a[i] -= a[k] * ti;
+            if ((ama & lbit) && lane <= i) a[i] -= a[ka] * ti;
           }
         }
-        if (am & lbit) a[k] = tmp;
+#pragma unroll
+        for (int i = SPLIT; i < km; i++) {
+          if ((amm >> i) & 1u) {
+            const double ti = tk[i];
+            if ((amm & lbit) && lane <= i) a[i] -= a[km] * ti;
+          }
+        }
+        if (ama & lbit) a[ka] = tmp;
+        if (amm & lbit) a[km] = tmp;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = K_NV - 1; k >= 0; k--) {
+      if (k < nv) {
+        double akk = rl(a[k], k);
+        if (akk < K_MINVAL) akk = K_MINVAL;
+        if (lane == k) a[k] = akk;
+        const unsigned int am = amask[k];
+        if (am) {
+          double tmp = a[k] / akk; /* lane i in anc(k): A[k][i] / A[k][k] */
+          /* the multipliers reach every lane through an LDS slot (broadcast reads) */
+          double* tk = R_SLOT(s, k & 1);
+          r_stage(tk, tmp);
+#pragma unroll
+          for (int i = 0; i < k; i++) {
+            if ((am >> i) & 1u) {
+              const double ti = tk[i];
+              if ((am & lbit) && lane <= i) a[i] -= a[k] * ti;
+            }
+          }
+          if (am & lbit) a[k] = tmp;
+        }
       }
     }
   }
@@ -988,13 +1035,32 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
     if (lane == i && i < nv) dg = a[i];
   const double dinv = 1.0 / dg;
   double x = lane < nv ? b : 0.0;
+  if constexpr (SPLIT > 0) {
+    /* the same pairing: x_i's updates come from its tree's descendants only, in descending order */
+    constexpr int NVS = KS::NV;
 #pragma unroll
-  for (int i = K_NV - 1; i >= 0; i--) {
-    if (i < nv) {
-      const unsigned int am = amask[i];
-      if (am) {
-        double xi = rl(x, i);
-        if (am & lbit) x -= a[i] * xi;
+    for (int t = 0; t < SPLIT; t++) {
+      const int ia = SPLIT - 1 - t, im0 = NVS - 1 - t;
+      const bool mcol = im0 >= SPLIT;
+      const int im = mcol ? im0 : 0;
+      const unsigned int ama = amask[ia], amm = mcol ? amask[im] : 0u;
+      if (ama | amm) {
+        const double xa = rl(x, ia);
+        const double xm = mcol ? rl(x, im) : 0.0;
+        const bool ua = (ama & lbit) != 0, um = (amm & lbit) != 0;
+        const double prod = ua ? a[ia] * xa : a[im] * xm;
+        if (ua || um) x -= prod;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = K_NV - 1; i >= 0; i--) {
+      if (i < nv) {
+        const unsigned int am = amask[i];
+        if (am) {
+          double xi = rl(x, i);
+          if (am & lbit) x -= a[i] * xi;
+        }
       }
     }
   }
@@ -1011,11 +1077,28 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   double r[K_NV];
 #pragma unroll
   for (int j = 0; j < K_NV; j++) r[j] = j <= col ? s.Hl[KTRI(col, j)] : 0.0;
+  if constexpr (SPLIT > 0) {
+    /* paired again: ancestor j of a lane is in the lane's own tree, ascending within it */
+    constexpr int NVS = KS::NV;
+    const bool lb = lane >= SPLIT;
 #pragma unroll
-  for (int j = 0; j < K_NV; j++) {
-    if (j < nv) {
-      double xj = rl(x, j);
-      if ((myam >> j) & 1u) x -= r[j] * xj;
+    for (int t = 0; t < SPLIT; t++) {
+      const int ja = t, jm0 = SPLIT + t;
+      const bool mcol = jm0 < NVS;
+      const int jm = mcol ? jm0 : 0;
+      const double xa = rl(x, ja);
+      const double xm = mcol ? rl(x, jm) : 0.0;
+      const bool ua = !lb && ((myam >> ja) & 1u), um = mcol && lb && ((myam >> jm) & 1u);
+      const double prod = ua ? r[ja] * xa : r[jm] * xm;
+      if (ua || um) x -= prod;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K_NV; j++) {
+      if (j < nv) {
+        double xj = rl(x, j);
+        if ((myam >> j) & 1u) x -= r[j] * xj;
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
