@@ -447,7 +447,18 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
       const double mass = m->body_mass[tid];
       sm[0] = xipos[0] * mass; sm[1] = xipos[1] * mass; sm[2] = xipos[2] * mass;
     }
-    r_subtree_sum<3, false>(m, sm);
+    if constexpr (KS::STATIC_TREE) {
+      /* the sums go through subtree_com's rows, components across lanes */
+      if (tid < nb)
+        for (int k = 0; k < 3; k++) s.subtree_com[tid][k] = sm[k];
+      SYNC();
+      r_subtree_sum_cols<3, false>(s.subtree_com, s.subtree_com);
+      if (tid < nb)
+        for (int k = 0; k < 3; k++) sm[k] = s.subtree_com[tid][k];
+      SYNC();
+    } else {
+      r_subtree_sum<3, false>(m, sm);
+    }
     if (tid < nb) {
       const int i = tid;
       if (m->body_subtreemass[i] < K_MINVAL) {
@@ -577,11 +588,16 @@ WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int nb = m->nbody, nv = NVOF(KS, m);
   if constexpr (NT == 64) {
     /* composite inertias summed up the tree in registers (lane = body) */
-    double crb[10];
-    for (int k = 0; k < 10; k++) crb[k] = tid < nb ? s.cinert[tid][k] : 0.0;
-    r_subtree_sum<10, true>(m, crb);
-    if (tid < nb)
-      for (int k = 0; k < 10; k++) s.u.body.b10[tid][k] = crb[k];
+    if constexpr (KS::STATIC_TREE) {
+      /* components across lanes: cinert rows in, crb rows out */
+      r_subtree_sum_cols<10, true>(s.cinert, s.u.body.b10);
+    } else {
+      double crb[10];
+      for (int k = 0; k < 10; k++) crb[k] = tid < nb ? s.cinert[tid][k] : 0.0;
+      r_subtree_sum<10, true>(m, crb);
+      if (tid < nb)
+        for (int k = 0; k < 10; k++) s.u.body.b10[tid][k] = crb[k];
+    }
     WT(34);
   } else {
     for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];

@@ -1133,6 +1133,32 @@ WD void r_subtree_sum(KModel m, double (&f)[C]) {
   }
 }
 
+/* main.xml (static body tree): the same subtree sums with the components across lanes.  Lane c < C
+   reads component c of every body from the LDS rows src[i][c] into registers, adds child into parent
+   for i = nb-1 .. 1 (the oracle's order; the parents are compile-time, so the adds are register to
+   register and only the tree's own dependencies order them) and writes the sums to dst[i][c] (src
+   and dst may be the same rows).  One pass of loads and stores instead of 20-24 readlane steps of C
+   doubles each.  The caller has made src visible (wave barrier); dst is visible on return. */
+template <int C, bool SKIP_WORLD, int SS, int DS>
+WD void r_subtree_sum_cols(const double (*src)[SS], double (*dst)[DS]) {
+  static_assert(C <= SS && C <= DS, "subtree sum: component count exceeds the row");
+  const int lane = w_lane();
+  if (lane < C) {
+    double F[UR3E_MAIN_NB];
+#pragma unroll
+    for (int i = 0; i < UR3E_MAIN_NB; i++) F[i] = src[i][lane];
+#pragma unroll
+    for (int i = UR3E_MAIN_NB - 1; i > 0; i--) {
+      const int p = ur3e_main_body_parent[i];
+      if (!SKIP_WORLD || p > 0) F[p] += F[i];
+    }
+#pragma unroll
+    for (int i = 0; i < UR3E_MAIN_NB; i++) dst[i][lane] = F[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 /* ================================================================== */
 /* body-tree passes for the compact tier (lane = body, nbody <= 64)    */
 /* ================================================================== */
@@ -1384,6 +1410,14 @@ WD void r_cfrc(KModel m, KS& s) {
     k_mul_inert_vec(f2, ci, cv);
     k_cross_force(f3, cv, f2);
     for (int r = 0; r < 6; r++) f[r] = f1[r] + f3[r];
+  }
+  if constexpr (KS::STATIC_TREE) {
+    if (lane < nb)
+      for (int r = 0; r < 6; r++) cfrc[lane][r] = f[r]; /* lane 0: the world's zeros */
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    r_subtree_sum_cols<6, true>(cfrc, cfrc);
+    return;
   }
 #pragma unroll
   for (int i = K_NB - 1; i > 0; i--) {
