@@ -1875,7 +1875,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) b->main_tree = 0;
   if (model->nbody != UR3E_MAIN_NB) b->main_tree = 0;
   for (int i = 0; i < model->nbody && b->main_tree; i++)
-    if (model->body_parentid[i] != ur3e_main_body_parent[i]) b->main_tree = 0;
+    if (model->body_parentid[i] != ur3e_main_body_parent[i] || model->body_dofnum[i] != ur3e_main_body_dofnum[i] ||
+        model->body_jntadr[i] != ur3e_main_body_jntadr[i])
+      b->main_tree = 0;
   for (int k = 0; k < 12; k++) {
     c.gains.task[k] = cfg->task_gains[k];
     c.gains.joint[k] = cfg->joint_gains[k];

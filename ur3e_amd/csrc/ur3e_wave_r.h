@@ -1302,6 +1302,32 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   asm volatile("" ::: "memory");
 }
 
+/* main.xml (static body tree): a root-to-leaf chain over the rows of a [body][6+] array with the six
+   components across lanes.  Row i holds body i's staged increment; lane c < 6 walks the bodies in
+   index order (parents first) in registers: ALL == false (velocities): V[i] = V[p] for a body
+   without dofs, V[p] + row[i] for a one-dof body, row[i] as staged for a several-dof body (a child
+   of the world, computed on its lane); ALL == true (accelerations): V[i] = V[p] + row[i] for every
+   body.  Row 0 (the world) is the start value.  The rows are overwritten with V. */
+template <bool ALL, int DS>
+WD void r_chain_cols(double (*rows)[DS]) {
+  const int lane = w_lane();
+  if (lane < 6) {
+    double V[UR3E_MAIN_NB];
+#pragma unroll
+    for (int i = 0; i < UR3E_MAIN_NB; i++) V[i] = rows[i][lane];
+#pragma unroll
+    for (int i = 1; i < UR3E_MAIN_NB; i++) {
+      const int p = ur3e_main_body_parent[i], dn = ur3e_main_body_dofnum[i];
+      if (ALL || dn == 1) V[i] = V[p] + V[i];
+      else if (dn == 0) V[i] = V[p];
+    }
+#pragma unroll
+    for (int i = 1; i < UR3E_MAIN_NB; i++) rows[i][lane] = V[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 /* w_com_vel fused with the forward (cacc) pass of w_rne_passive: both only need the parent's
    values, so one level sweep produces cvel, cdof_dot and cacc */
 template <class KS>
@@ -1336,42 +1362,69 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const bool one = bdn == 1 && jt != UR3E_JNT_FREE;
   double cqv[6], cvp[6] = {0, 0, 0, 0, 0, 0}, tmp[6] = {0, 0, 0, 0, 0, 0};
   for (int r = 0; r < 6; r++) cqv[r] = cd[r] * qv;
-  for (int lvl = 1; lvl <= nlevel; lvl++) {
-    if (depth == lvl) {
-      double cv[6];
-      for (int k = 0; k < 6; k++) cv[k] = s.cvel[pid][k];
-      if (one) {
-        for (int r = 0; r < 6; r++) { cvp[r] = cv[r]; cv[r] += cqv[r]; }
+  /* general body (free joint, several dofs, none): w_com_vel on cv (the parent's cvel), and its cacc
+     term in tmp */
+  auto general = [&](double (&cv)[6]) {
+    for (int j = 0; j < bdn; j++) {
+      int dof = bda + j;
+      int jtj = onejnt ? jt : m->jnt_type[m->dof_jntid[dof]];
+      if (jtj == UR3E_JNT_FREE) {
+        for (int k = 0; k < 3; k++)
+          for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
+        double tq[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < 3; k++)
+          for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+        for (int r = 0; r < 6; r++) cv[r] += tq[r];
+        for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
+        for (int r = 0; r < 6; r++) tq[r] = 0;
+        for (int k = 3; k < 6; k++)
+          for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
+        for (int r = 0; r < 6; r++) cv[r] += tq[r];
+        j += 5;
       } else {
-        /* general body (free joint, several dofs, none): w_com_vel, and its cacc term */
-        for (int j = 0; j < bdn; j++) {
-          int dof = bda + j;
-          int jtj = onejnt ? jt : m->jnt_type[m->dof_jntid[dof]];
-          if (jtj == UR3E_JNT_FREE) {
-            for (int k = 0; k < 3; k++)
-              for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
-            double tq[6] = {0, 0, 0, 0, 0, 0};
-            for (int k = 0; k < 3; k++)
-              for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
-            for (int r = 0; r < 6; r++) cv[r] += tq[r];
-            for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
-            for (int r = 0; r < 6; r++) tq[r] = 0;
-            for (int k = 3; k < 6; k++)
-              for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
-            for (int r = 0; r < 6; r++) cv[r] += tq[r];
-            j += 5;
-          } else {
-            k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
-            for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
-          }
-        }
-        for (int j = 0; j < bdn; j++)
-          for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+        k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
+        for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
       }
+    }
+    for (int j = 0; j < bdn; j++)
+      for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+  };
+  /* main.xml: the two chains with the components across lanes (r_chain_cols), the several-dof bodies
+     (children of the world without children of their own, checked by the generator) on their lanes
+     first.  Same expressions, same operands: bit-identical. */
+  constexpr bool COLS = KS::STATIC_TREE && UR3E_MAIN_BODY_COLS;
+  if constexpr (COLS) {
+    if (depth == 1 && bdn > 1) {
+      double cv[6];
+      for (int k = 0; k < 6; k++) cv[k] = s.cvel[0][k];
+      general(cv);
       for (int k = 0; k < 6; k++) s.cvel[lane][k] = cv[k];
     }
+    if (depth > 0 && one)
+      for (int k = 0; k < 6; k++) s.cvel[lane][k] = cqv[k]; /* staged increment */
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    r_chain_cols<false>(s.cvel);
+    if (depth > 0 && one)
+      for (int k = 0; k < 6; k++) cvp[k] = s.cvel[pid][k];
+  } else {
+    /* Split like r_kinematics: the velocity chain cvel = parent cvel + cdof * qvel runs level by level,
+       then cdof_dot and the acceleration term of every single-dof body are formed at once, then the
+       chain cacc = parent cacc + term.  Same expressions, same operands: bit-identical. */
+    for (int lvl = 1; lvl <= nlevel; lvl++) {
+      if (depth == lvl) {
+        double cv[6];
+        for (int k = 0; k < 6; k++) cv[k] = s.cvel[pid][k];
+        if (one) {
+          for (int r = 0; r < 6; r++) { cvp[r] = cv[r]; cv[r] += cqv[r]; }
+        } else {
+          general(cv);
+        }
+        for (int k = 0; k < 6; k++) s.cvel[lane][k] = cv[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
   }
   WT(31);
   if (depth > 0 && one) {
@@ -1380,12 +1433,20 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
     for (int r = 0; r < 6; r++) s.cdof_dot[bda][r] = cdd[r];
     for (int r = 0; r < 6; r++) tmp[r] += cdd[r] * qv;
   }
-  for (int lvl = 1; lvl <= nlevel; lvl++) {
-    if (depth == lvl) {
-      for (int k = 0; k < 6; k++) cacc[lane][k] = cacc[pid][k] + tmp[k];
-    }
+  if constexpr (COLS) {
+    if (depth > 0)
+      for (int k = 0; k < 6; k++) cacc[lane][k] = tmp[k]; /* staged term (the world's row is set) */
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    r_chain_cols<true>(cacc);
+  } else {
+    for (int lvl = 1; lvl <= nlevel; lvl++) {
+      if (depth == lvl) {
+        for (int k = 0; k < 6; k++) cacc[lane][k] = cacc[pid][k] + tmp[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
   }
 }
 
