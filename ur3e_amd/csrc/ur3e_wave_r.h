@@ -1263,25 +1263,63 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
     k_mat_vec3(tv, pm, bpos);
   }
   /* 3. position chain */
-  for (int lvl = 1; lvl <= nlevel; lvl++) {
-    if (depth == lvl) {
-      double xpos[3];
+  if constexpr (KS::STATIC_TREE && UR3E_MAIN_BODY_COLS) {
+    /* main.xml: with the components across lanes.  Each body stages its terms -- tv in its xpos row,
+       ra in its joint's xanchor row, vec in its joint's qloc row (unused by this path); a free body
+       (a child of the world) its final position -- then lane c < 3 walks the bodies in index order
+       in registers: P = parent + tv, and for a hinge anchor = ra + P, P = anchor - vec. */
+    if (depth > 0) {
       if (isfree) {
-        xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
-        s.xanchor[jf][0] = xpos[0]; s.xanchor[jf][1] = xpos[1]; s.xanchor[jf][2] = xpos[2];
+        for (int c = 0; c < 3; c++) { s.xpos[lane][c] = s.qpos[qa + c]; s.xanchor[jf][c] = s.qpos[qa + c]; }
       } else {
-        for (int c = 0; c < 3; c++) xpos[c] = s.xpos[pid][c] + tv[c];
-        if (jn == 1) {
-          double xanchor[3];
-          for (int c = 0; c < 3; c++) xanchor[c] = ra[c] + xpos[c];
-          for (int c = 0; c < 3; c++) xpos[c] = xanchor[c] - vec[c];
-          for (int c = 0; c < 3; c++) s.xanchor[jf][c] = xanchor[c];
-        }
+        for (int c = 0; c < 3; c++) s.xpos[lane][c] = tv[c];
+        if (jn == 1)
+          for (int c = 0; c < 3; c++) { s.xanchor[jf][c] = ra[c]; s.qloc[jf][c] = vec[c]; }
       }
-      for (int c = 0; c < 3; c++) s.xpos[lane][c] = xpos[c];
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    if (lane < 3) {
+      double P[UR3E_MAIN_NB];
+#pragma unroll
+      for (int i = 0; i < UR3E_MAIN_NB; i++) P[i] = s.xpos[i][lane];
+#pragma unroll
+      for (int i = 1; i < UR3E_MAIN_NB; i++) {
+        const int p = ur3e_main_body_parent[i], dn = ur3e_main_body_dofnum[i], j = ur3e_main_body_jntadr[i];
+        if (dn == 0) {
+          P[i] = P[p] + P[i];
+        } else if (dn == 1) {
+          const double xa = s.xanchor[j][lane] + (P[p] + P[i]);
+          P[i] = xa - s.qloc[j][lane];
+          s.xanchor[j][lane] = xa;
+        }
+      }
+#pragma unroll
+      for (int i = 1; i < UR3E_MAIN_NB; i++) s.xpos[i][lane] = P[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    for (int lvl = 1; lvl <= nlevel; lvl++) {
+      if (depth == lvl) {
+        double xpos[3];
+        if (isfree) {
+          xpos[0] = s.qpos[qa]; xpos[1] = s.qpos[qa + 1]; xpos[2] = s.qpos[qa + 2];
+          s.xanchor[jf][0] = xpos[0]; s.xanchor[jf][1] = xpos[1]; s.xanchor[jf][2] = xpos[2];
+        } else {
+          for (int c = 0; c < 3; c++) xpos[c] = s.xpos[pid][c] + tv[c];
+          if (jn == 1) {
+            double xanchor[3];
+            for (int c = 0; c < 3; c++) xanchor[c] = ra[c] + xpos[c];
+            for (int c = 0; c < 3; c++) xpos[c] = xanchor[c] - vec[c];
+            for (int c = 0; c < 3; c++) s.xanchor[jf][c] = xanchor[c];
+          }
+        }
+        for (int c = 0; c < 3; c++) s.xpos[lane][c] = xpos[c];
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
   }
   WT(30);
   if (lane < nfr) {
