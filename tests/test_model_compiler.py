@@ -83,7 +83,10 @@ def test_generated_main_tree_matches_model():
     from ur3e_amd import _build
     path = _build.gen_main_tree()
     txt = open(path).read()
-    masks = [int(x, 16) for x in re.findall(r"0x([0-9a-f]+)u", txt)]
+    def arr(name):
+        body = re.search(name + r"\[\d+\] = \{([^}]*)\}", txt).group(1)
+        return [int(x.strip().rstrip("ul"), 0) for x in body.split(",")]
+    masks = arr("ur3e_main_dof_anc_mask")
     md = load_json(os.path.join(ASSETS, "main.model.json"))
     par = md["dof_parentid"][:md["nv"]]
     want = []
@@ -94,3 +97,8 @@ def test_generated_main_tree_matches_model():
             j = par[j]
         want.append(m)
     assert masks == want
+    nb = md["nbody"]
+    bpar = md["body_parentid"][:nb]
+    assert arr("ur3e_main_body_parent") == bpar
+    assert arr("ur3e_main_body_dofnum") == md["body_dofnum"][:nb]
+    assert arr("ur3e_main_body_jntadr") == md["body_jntadr"][:nb]

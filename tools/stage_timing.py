@@ -8,10 +8,12 @@ usage: stage_timing.py [n_envs] [envs_per_block] [workload: gym | c3] [tier: 0 c
 import ctypes, os, subprocess, sys
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, REPO)
-LIB = os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_timing.so")
+# UR3E_TIMING_LIB / UR3E_TIMING_FLAGS: a second diagnostic variant (its own library, extra -D flags)
+LIB = os.environ.get("UR3E_TIMING_LIB", os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd_timing.so"))
 if not os.path.exists(LIB):
     from ur3e_amd import _build  # same flags as the product library (incl. -disable-machine-licm)
-    subprocess.run([_build.HIPCC] + _build.FLAGS + ["-DUR3E_STAGE_TIMING", "-DW_SMALL_MAXCON=9", "-o", LIB,
+    extra = os.environ.get("UR3E_TIMING_FLAGS", "").split()
+    subprocess.run([_build.HIPCC] + _build.FLAGS + extra + ["-DUR3E_STAGE_TIMING", "-DW_SMALL_MAXCON=9", "-o", LIB,
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_batch.hip"),
                     os.path.join(REPO, "ur3e_amd", "csrc", "ur3e_vecnorm.hip")], check=True)
 os.environ["UR3E_LIB"] = LIB
