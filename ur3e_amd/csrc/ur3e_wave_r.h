@@ -985,18 +985,22 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
         const double tmp = (lb ? a[km] : a[ka]) / (lb ? akkm : akka);
         double* tk = R_SLOT(s, t & 1);
         r_stage(tk, tmp);
+        /* every lane updates, without the lane-in-anc(k) and lane <= i masks: a lane outside them
+           holds, in row i, an element no later step reads (upper triangle, or a column that is not
+           an ancestor of row i: the factor, the sweeps and the transpose below only read ancestor
+           pairs and the diagonal) */
 #pragma unroll
         for (int i = 0; i < ka; i++) {
           if ((ama >> i) & 1u) {
             const double ti = tk[i];
-            if ((ama & lbit) && lane <= i) a[i] -= a[ka] * ti;
+            a[i] -= a[ka] * ti;
           }
         }
 #pragma unroll
         for (int i = SPLIT; i < km; i++) {
           if ((amm >> i) & 1u) {
             const double ti = tk[i];
-            if ((amm & lbit) && lane <= i) a[i] -= a[km] * ti;
+            a[i] -= a[km] * ti;
           }
         }
         if (ama & lbit) a[ka] = tmp;
