@@ -1,4 +1,4 @@
-"""r_div_rcp (ur3e_amd/csrc/ur3e_wave_r.h), the Newton triangular sweeps' division by the Cholesky
+"""k_div_rcp (ur3e_amd/csrc/ur3e_engine.h), the Newton triangular sweeps' division by the Cholesky
 pivot from its reciprocal, is the correctly rounded quotient: tools/div_rcp_check.c compares it with
 n / d bit for bit on the host (the GPU sweeps are compared with the oracle by the -m gpu parity tests)."""
 import os

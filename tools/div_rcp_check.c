@@ -1,4 +1,4 @@
-/* Host check of r_div_rcp (ur3e_amd/csrc/ur3e_wave_r.h): with r = 1.0 / d and q0 = n * r,
+/* Host check of k_div_rcp (ur3e_amd/csrc/ur3e_engine.h): with r = 1.0 / d and q0 = n * r,
    fma(-fma(d, q0, -n), r, q0) == n / d bit for bit (signed zeros included), d > 0.
    Operands: random across 120 binades of n and 60 of d (signed zeros every 17th pair), then
    structured pairs (integers, d near 1 and near powers of two, quotients near representable values).

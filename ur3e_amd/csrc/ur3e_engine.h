@@ -57,6 +57,18 @@
 
 #define KD __device__ static inline
 #define KDN __device__ static __attribute__((noinline))
+/* n / d from r = 1.0 / d (itself a correctly rounded division), d > 0 finite: q0 = n r is within an
+   ulp of n / d, the residual d q0 - n is exact in one fma, and q0 - e r rounds to the correctly rounded
+   quotient (Markstein's theorem: r within half an ulp of 1/d, q0 within an ulp of n/d; no underflow or
+   overflow).  Signed zeros: n = -0 gives q0 = -0, e = +0, -0 - (+0) r = -0, as -0 / d.  Three
+   operations instead of the ~11 of a full division, so several quotients by one divisor cost one
+   division and three operations each.  tools/div_rcp_check.c checks it against n / d over 6e8 random
+   and structured operand pairs (tests/test_div_rcp.py). */
+KD double k_div_rcp(double n, double d, double r) {
+  const double q0 = n * r;
+  const double e = __builtin_fma(d, q0, -n);
+  return __builtin_fma(-e, r, q0);
+}
 /* this lane's index within the workgroup, opaque to the optimiser: a value derived from
    threadIdx.x alone is loop-invariant, and LICM would hoist all of them out of the per-substep
    loop and keep them live (spilled) across the whole forward pass; reading the lane through an
@@ -196,7 +208,10 @@ KD void k_normalize4(double q[4]) {
   double ra = a, rb = b, rc = c, rd = d;
   /* the divisions stay behind a branch (skipped when no lane needs them: an already unit
      quaternion, the common case); only scalars are assigned in it */
-  if (!tiny && fabs(n - 1.0) > K_MINVAL) { ra = a / n; rb = b / n; rc = c / n; rd = d / n; }
+  if (!tiny && fabs(n - 1.0) > K_MINVAL) {
+    const double r = 1.0 / n;
+    ra = k_div_rcp(a, n, r); rb = k_div_rcp(b, n, r); rc = k_div_rcp(c, n, r); rd = k_div_rcp(d, n, r);
+  }
   q[0] = tiny ? 1.0 : ra;
   q[1] = tiny ? 0.0 : rb;
   q[2] = tiny ? 0.0 : rc;
@@ -208,7 +223,10 @@ KD double k_normalize3(double v[3]) {
   double n = sqrt(a * a + b * b + c * c);
   const bool tiny = n < K_MINVAL;
   double ra = 1, rb = 0, rc = 0;
-  if (!tiny) { ra = a / n; rb = b / n; rc = c / n; }
+  if (!tiny) {
+    const double r = 1.0 / n;
+    ra = k_div_rcp(a, n, r); rb = k_div_rcp(b, n, r); rc = k_div_rcp(c, n, r);
+  }
   v[0] = tiny ? 1.0 : ra;
   v[1] = tiny ? 0.0 : rb;
   v[2] = tiny ? 0.0 : rc;
@@ -672,7 +690,8 @@ __device__ static __forceinline__ int k_box_box_t(const double p1[3], const doub
       k_cross3(u, a[i], b[j]);
       double len = sqrt(k_dot3(u, u));
       if (len < 1e-6) continue;
-      u[0] /= len; u[1] /= len; u[2] /= len;
+      const double rlen = 1.0 / len;
+      u[0] = k_div_rcp(u[0], len, rlen); u[1] = k_div_rcp(u[1], len, rlen); u[2] = k_div_rcp(u[2], len, rlen);
       double ext = 0;
 #pragma unroll
       for (int k = 0; k < 3; k++) ext += s1[k] * fabs(k_dot3(a[k], u));

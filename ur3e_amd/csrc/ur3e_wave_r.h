@@ -29,17 +29,6 @@ __device__ __forceinline__ double rl(double v, int lane) {
   return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo));
 }
 __device__ __forceinline__ int rli(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
-/* n / d from r = 1.0 / d (itself a correctly rounded division), d > 0 finite: q0 = n r is within an
-   ulp of n / d, the residual d q0 - n is exact in one fma, and q0 - e r rounds to the correctly rounded
-   quotient (Markstein's theorem: r within half an ulp of 1/d, q0 within an ulp of n/d; no underflow or
-   overflow).  Signed zeros: n = -0 gives q0 = -0, e = +0, -0 - (+0) r = -0, as -0 / d.  Three
-   operations instead of the ~11 of a full division.  tools/div_rcp_check.c checks it against n / d
-   over 6e8 random and structured operand pairs. */
-__device__ __forceinline__ double r_div_rcp(double n, double d, double r) {
-  const double q0 = n * r;
-  const double e = __builtin_fma(d, q0, -n);
-  return __builtin_fma(-e, r, q0);
-}
 /* per-lane source (ds_bpermute) */
 __device__ __forceinline__ double shf(double v, int src) {
   long long b = __builtin_bit_cast(long long, v);
@@ -631,8 +620,8 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   /* Both sweeps divide by L[k][k] (>= sqrt(K_MINVAL) > 0).  Lane k divides its own tmp by its own
-     pivot and the quotient is read back from lane k: tmp / L[k][k] as r_div_rcp's three operations
-     with the pivot's reciprocal taken once (r_div_rcp: correctly rounded, so the same bits as the
+     pivot and the quotient is read back from lane k: tmp / L[k][k] as k_div_rcp's three operations
+     with the pivot's reciprocal taken once (k_div_rcp: correctly rounded, so the same bits as the
      oracle's division) instead of a full division sequence on the uniform operands per step */
   const double dg = lane < nv ? s.Hl[KTRI(row, row)] : 1.0;
   const double rdg = 1.0 / dg;
@@ -643,7 +632,7 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
 #pragma unroll
   for (int k = 0; k < K_NV; k++) {
     if (k < nv) {
-      double xk = rl(r_div_rcp(tmp, dg, rdg), k);
+      double xk = rl(k_div_rcp(tmp, dg, rdg), k);
       yf = lane == k ? xk : yf;
       tmp -= h[k] * xk;
     }
@@ -661,7 +650,7 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
 #pragma unroll
   for (int i = K_NV - 1; i >= 0; i--) {
     if (i < nv) {
-      double xi = rl(r_div_rcp(tmp, dg, rdg), i); /* lane i: lt[i] = L[i][i] = dg */
+      double xi = rl(k_div_rcp(tmp, dg, rdg), i); /* lane i: lt[i] = L[i][i] = dg */
       xf = lane == i ? xi : xf;
       tmp -= lt[i] * xi;
     }
