@@ -35,14 +35,18 @@ ALGO_BYTES_PER_ENV_STEP = 1898
 FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
-def _profile_file(kind: str) -> str:
-    """profiles/<kind>_rNN.json of the latest round that has one (traffic: PMC HBM bytes per launch of
-    the step kernel; flops: the oracle-counted FP64 flops per env-step)"""
-    for r in ("r02", "r01"):
-        p = os.path.join(REPO, "profiles", f"{kind}_{r}.json")
-        if os.path.exists(p):
-            return p
-    return os.path.join(REPO, "profiles", f"{kind}_r01.json")
+def _profile_file(kind: str):
+    """profiles/<kind>_rNN.json of the newest round that has one (traffic: PMC HBM bytes per launch of
+    the step kernel; flops: the oracle-counted FP64 flops per env-step), or None.  Each file records the
+    commit it was measured at (`head`); the GPU box has no .git, so the newest round is the selector."""
+    import re
+    best, best_r = None, -1
+    d = os.path.join(REPO, "profiles")
+    for f in os.listdir(d) if os.path.isdir(d) else ():
+        m = re.fullmatch(rf"{kind}_r(\d+)\.json", f)
+        if m and int(m.group(1)) > best_r:
+            best, best_r = os.path.join(d, f), int(m.group(1))
+    return best
 
 
 def _state_diff(gb, ob):
@@ -75,13 +79,83 @@ def _host_threads() -> int:
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_core_steps=400):
+def _host_info() -> dict:
+    """The machine the CPU baseline ran on: logical CPUs of the machine, of this process's affinity mask,
+    and lscpu's model / socket / core / thread counts."""
+    info = {"machine_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        want = {"Model name": "lscpu_model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "CPU(s)": "lscpu_cpus"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in want:
+                info[want[k.strip()]] = v.strip()
+    except Exception as e:  # lscpu missing: the cpuinfo model is still reported
+        info["lscpu"] = f"unavailable: {e}"
+    return info
+
+
+def _time_oracle(ob, actions_fn, steps):
+    """seconds of oracle stepping over `steps` batches of actions_fn(i) (action generation untimed)"""
+    dt = 0.0
+    for i in range(steps):
+        a = actions_fn(i)
+        t0 = time.perf_counter()
+        ob.step(a)
+        dt += time.perf_counter() - t0
+    return dt
+
+
+def cpu_other_configs(L, threads, c2_envs=4096, c2_steps=200, c3_envs=1024, c3_rows=(1500, 1800)):
+    """Oracle CPU figures for the other single-GPU configs, on `threads` host threads:
+    C2 -- ur3e_2f85, random joint targets through move_j's PD (as other_configs);
+    C3 -- main.xml move_l_mug scripted pick, the rows c3_rows of the grasp window (reached untimed)."""
+    from oracle import pyoracle as po
+    from ur3e_amd import runtime as rt
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    L.ur3o_set_threads(threads)
+    out = {}
+    md, mc = rt.load_model("ur3e_2f85")
+    cfg = rt.make_config(task=rt.TASK_MOVE_J, frame_skip=1, model=md, seed=3, reset_noise=False,
+                         reset_key=md["id_key_down"])
+    ob = po.OracleBatch(mc, po.config_from(cfg), c2_envs, L=L)
+    q0 = np.array(md["key_qpos"][md["id_key_down"]][:6])
+    rng = np.random.default_rng(3)
+
+    def act(_):
+        a = np.empty((c2_envs, 7))
+        a[:, :6] = q0 + rng.uniform(-0.5, 0.5, size=(c2_envs, 6))
+        a[:, 6] = rng.uniform(0, 1, size=c2_envs)
+        return a
+    dt = _time_oracle(ob, act, c2_steps)
+    out["C2_ur3e_2f85_move_j"] = {"value": c2_envs * c2_steps / dt, "unit": "env-steps/s", "cores": threads,
+                                  "sample": f"{c2_envs} envs x {c2_steps} move_j env-steps, {dt:.1f} s"}
+    drv = MoveLMug(c3_envs, reset_mode="low", seed=0)   # trajectory rows only (evaluated on the GPU)
+    ob = po.OracleBatch(drv.batch.model_c, po.config_from(drv.batch.cfg), c3_envs, L=L)
+    g0, g1 = c3_rows
+    for t in range(g0):
+        ob.step(drv.traj.row(t).cpu().numpy())
+    rows = [drv.traj.row(t).cpu().numpy() for t in range(g0, g1)]
+    dt = _time_oracle(ob, lambda i: rows[i], g1 - g0)
+    drv.close()
+    out["C3_main_move_l_mug"] = {"value": c3_envs * (g1 - g0) / dt, "unit": "env-steps/s", "cores": threads,
+                                 "sample": f"{c3_envs} envs x rows {g0}-{g1} of the scripted pick (grasp window, "
+                                           f"reached untimed), {dt:.1f} s"}
+    return out
+
+
+def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_core_steps=400,
+                 all_cores_steps=300):
     """The cpu_baseline leg.  The oracle (oracle/, the same algorithm in C) is compiled for this host
     (-O3 -march=native -ffp-contract=off, OpenMP over envs) and timed on a bounded sample of the bench
-    workload: (1) all host threads: n_envs_sample gym ur3e-v2 envs x `steps` env-steps; (2) one thread:
-    one_core_envs x one_core_steps.  As the checker, the same seeded actions are replayed through a
-    fresh GPU handle, giving the metric's second half, max |qpos - ref| after `steps` env-steps (the
-    oracle is the reference here: MuJoCo is absent)."""
+    workload: (1) this process's CPU share (OMP_NUM_THREADS, 16 per GPU on the box): n_envs_sample gym
+    ur3e-v2 envs x `steps` env-steps; (2) every core of the affinity mask: n_envs_sample x all_cores_steps;
+    (3) one thread: one_core_envs x one_core_steps; (4) C2 and C3 on the CPU share.  As the checker, the
+    same seeded actions of (1) are replayed through a fresh GPU handle, giving the metric's second half,
+    max |qpos - ref| after `steps` env-steps (the oracle is the reference here: MuJoCo is absent)."""
     import tempfile
 
     import torch
@@ -119,15 +193,34 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         t0 = time.perf_counter()
         ob1.step(a)
         dt1 += time.perf_counter() - t0
+    # (3) every core of the affinity mask (the machine's cores the process may run on)
+    host = _host_info()
+    n_all = min(host["affinity_cpus"], 512)  # threads count against the box's task limit
+    all_cores = None
+    if n_all != threads:
+        L.ur3o_set_threads(n_all)
+        oba = po.OracleBatch(mc, po.config_from(c), n_envs_sample, L=L)
+        rng = np.random.default_rng(seed + 2)
+        dta = _time_oracle(oba, lambda _: rng.uniform(lo, hi, size=(n_envs_sample, 4)), all_cores_steps)
+        del oba
+        all_cores = {"value": n_envs_sample * all_cores_steps / dta, "unit": "env-steps/s", "cores": n_all,
+                     "sample": f"{n_envs_sample} envs x {all_cores_steps} env-steps from reset, OpenMP {n_all} "
+                               f"threads (every CPU of the affinity mask), {dta:.1f} s"}
     L.ur3o_set_threads(threads)
+    try:
+        others = cpu_other_configs(L, threads)
+    except Exception as e:  # secondary figures never fail the baseline
+        others = {"error": repr(e)}
     cpu = _cpu_model()
     build = "gcc -O3 -march=native -ffp-contract=off -fopenmp (compiled on this host)"
     base = dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=threads, kind="port",
                 sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps) from reset, "
-                       f"oracle/ C restatement, OpenMP {threads} threads, {dt:.1f} s",
-                cpu_model=cpu, build=build,
+                       f"oracle/ C restatement, OpenMP {threads} threads (this process's CPU share), {dt:.1f} s",
+                cpu_model=cpu, build=build, host=host,
+                all_cores=all_cores,
                 one_core={"value": one_core_envs * one_core_steps / dt1, "unit": "env-steps/s", "cores": 1,
-                          "sample": f"{one_core_envs} envs x {one_core_steps} env-steps, 1 thread, {dt1:.1f} s"})
+                          "sample": f"{one_core_envs} envs x {one_core_steps} env-steps, 1 thread, {dt1:.1f} s"},
+                other_configs=others)
     return base, parity
 
 
@@ -393,24 +486,28 @@ def main():
 
     if rank == 0:
         achieved = ALGO_BYTES_PER_ENV_STEP * n / (step_kernel_ms * 1e-3) / 1e9
-        prof_traffic = None
+        prof_traffic, traffic_src = None, None
         tf = _profile_file("traffic")
-        if os.path.exists(tf):
+        if tf:
             try:
                 with open(tf) as f:
-                    prof_traffic = json.load(f).get("hbm_bytes_per_launch")
+                    tj = json.load(f)
+                prof_traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = {"file": os.path.relpath(tf, REPO), "pmc": tj.get("source"), "head": tj.get("head")}
             except Exception:
                 prof_traffic = None
         fp64 = None
         ff = _profile_file("flops")
-        if os.path.exists(ff):
+        if ff:
             try:
                 with open(ff) as f:
-                    fpe = json.load(f)["flops_per_env_step"]
+                    fj = json.load(f)
+                fpe = fj["flops_per_env_step"]
                 ach = fpe * n / (step_kernel_ms * 1e-3) / 1e12
                 fp64 = {"bound": "fp64-vector", "achieved": ach, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": ach / FP64_VECTOR_PEAK_TFLOPS, "flops_per_env_step": fpe,
-                        "source": os.path.relpath(ff, REPO) + " (tools/count_flops.py: counting build of the oracle)"}
+                        "source": os.path.relpath(ff, REPO) + " (tools/count_flops.py: counting build of the oracle)",
+                        "head": fj.get("head")}
             except Exception:
                 fp64 = None
         cpu, parity = None, None
@@ -459,7 +556,7 @@ def main():
                                        "env_steps_since_reset": [0, n_fresh],
                                        "note": "rank-0 stream time of the first env-steps after reset"}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic, "traffic_source": traffic_src,
                          "kernel": batch_kinfo["kernel"] + " + w_env_step_list<128> fallback",
                          "kernel_ms": step_kernel_ms,
                          "stream_avg_ms": kernel_avg_ms,

@@ -199,6 +199,13 @@ int ur3e_batch_queue_stats(ur3e_batch_t* b, unsigned long long* stats);
    static first units, so every one of them is claimed and run by its consumer */
 int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int leave_static_units);
 
+/* diagnostic (the queue's forward-progress test): launch `workgroups` workgroups on `stream` that each
+   hold 64 KB of LDS (two per CU leave room for one step workgroup) for hold_us microseconds, and
+   return once they have all started (started = how many had, waited for at most 2 * hold_us), so
+   that work launched next on another stream finds most of its workgroup slots taken.  Every
+   workgroup exits after hold_us; results of other work never change. */
+int ur3e_debug_hold_slots(int device, int workgroups, int hold_us, void* stream, int* started);
+
 /* the step kernel this handle launches: 0 compact tier, one workgroup per env-step; 1 compact tier
    as a substep work queue; 2 full-capacity tier only; 3 one env per lane (v1) */
 int ur3e_batch_schedule(const ur3e_batch_t* b);

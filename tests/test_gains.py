@@ -65,3 +65,40 @@ def test_malformed_sections_raise(tmp_path):
         gains.joint_gains(str(p))
     with pytest.raises(FileNotFoundError):
         gains.task_gains(str(tmp_path / "missing.yml"))
+
+
+def test_make_config_reads_move_j_move_l_yaml(tmp_path):
+    """move_j / move_l configs take their pd_joint_ctrl gains from config_j.yml / config_l.yml
+    (move_j.py:46-52, move_l.py:92-99) when none are given, and from an explicit path when one is."""
+    cj = rt.make_config(task=rt.TASK_MOVE_J)
+    assert list(cj.joint_gains) == gains.joint_gains()["kp"] + gains.joint_gains()["kd"]
+    p = tmp_path / "j.yml"
+    _write(p, dict(hold=100, qpos=dict(kp=[1.0, 2.0, 3.0, 4.0, 5.0, 6.0], kd=[0.5] * 6)))
+    cj = rt.make_config(task=rt.TASK_MOVE_J, config_yaml_path=str(p))
+    assert list(cj.joint_gains) == [1.0, 2.0, 3.0, 4.0, 5.0, 6.0] + [0.5] * 6
+    p = tmp_path / "l.yml"
+    _write(p, dict(hold=100, pos=dict(kp=[7.0] * 6, kd=[8.0] * 6), rot=dict(kp=[9.0] * 6, kd=[10.0] * 6)))
+    cl = rt.make_config(task=rt.TASK_MOVE_L, config_yaml_path=str(p))
+    assert list(cl.joint_gains) == [7.0] * 6 + [8.0] * 6
+    assert list(cl.rot_joint_gains) == [9.0] * 6 + [10.0] * 6
+    # explicit gains still win
+    cl = rt.make_config(task=rt.TASK_MOVE_L, joint_gains=dict(kp=[1.0] * 6, kd=[2.0] * 6), config_yaml_path=str(p))
+    assert list(cl.joint_gains) == [1.0] * 6 + [2.0] * 6 and list(cl.rot_joint_gains) == [9.0] * 6 + [10.0] * 6
+
+
+def test_output_buffers_checked_before_launch():
+    """Batch.out_ptr (used by get_actuator_force(out) and task_space_state(batch, out)) rejects a buffer
+    the kernel would write out of bounds: wrong dtype, shape, device or a non-contiguous view."""
+    import types
+
+    import torch
+    fake = types.SimpleNamespace(torch=torch, device=torch.device("cpu"), n=4)
+    ok = torch.zeros((4, 7), dtype=torch.float64)
+    assert rt.Batch.out_ptr(fake, ok, 7, "t").value == ok.data_ptr()
+    rec = torch.zeros((3, 4, 7), dtype=torch.float64)
+    assert rt.Batch.out_ptr(fake, rec[1], 7, "t").value == rec[1].data_ptr()  # a row of a recording buffer
+    for bad in (torch.zeros((4, 7), dtype=torch.float32), torch.zeros((4, 6), dtype=torch.float64),
+                torch.zeros((3, 7), dtype=torch.float64), torch.zeros((7, 4), dtype=torch.float64).t(),
+                torch.zeros((4, 7), dtype=torch.float64, device="meta"), ok.numpy()):
+        with pytest.raises(ValueError):
+            rt.Batch.out_ptr(fake, bad, 7, "t")

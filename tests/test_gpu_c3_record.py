@@ -47,3 +47,58 @@ def test_move_l_mug_records_every_row_bit_exact():
     st = task_space_state(gb)
     np.testing.assert_array_equal(st.cpu().numpy(), tt[-1])
     drv.close()
+
+
+def test_grasp_flag_set_from_pad_contact_states():
+    """The grasp-contact column of traj_true (get_boolean_grasp_contact, utils/utils.py:236-243: the
+    (left, right) pad1 touch pair compared lexicographically with (0.1, 0.1)) in its 1 branch.  The
+    scripted pick on the box-surrogate pads rarely lands contacts inside the 0.5 mm pad1 site boxes, so
+    the states come from tests/golden/touch_states.npz (fish on a pad face, pad as geom A and as geom B,
+    pinned by tests/test_touch_states.py): set through ur3e_batch_set_state on a move_l_mug (TRAJ_L)
+    handle, then 30 rows holding the tcp pose with the gripper closing.  traj_true is read on the device
+    and compared with the oracle every row; the 1 branch must be produced, and the 0 branch beside it."""
+    import os
+
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import pyoracle as po
+    from ur3e_amd import gains
+    from ur3e_amd import runtime as rt
+    from ur3e_amd.controller.move_l_mug import task_space_state
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "touch_states.npz"))
+    names = ["right_face", "left_face", "left_geom_b"]
+    reps = 4
+    q = np.concatenate([np.tile(z[nm], (reps, 1)) for nm in names])
+    v = np.concatenate([np.tile(z[nm + "_qvel"], (reps, 1)) for nm in names])
+    n = len(q)
+    md, mc = rt.load_model("main")
+    cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
+                         reset_noise="low", reset_key=md["id_key_down"], model=md, seed=2,
+                         task_gains=gains.task_gains())
+    gb = rt.Batch(mc, cfg, n)
+    ob = po.OracleBatch(mc, po.config_from(cfg), n)
+    tl, tr = gb.touch_index("left"), gb.touch_index("right")
+    gb.set_state(q, v)
+    ob.set_state(q, v)
+    st = task_space_state(gb).cpu().numpy()
+    np.testing.assert_array_equal(st, ob.task_space_state(tl, tr))
+    touch = gb.get_touch().cpu().numpy()
+    lex = np.array([(a, b) > (0.1, 0.1) for a, b in zip(touch[:, tl], touch[:, tr])], dtype=np.float64)
+    np.testing.assert_array_equal(st[:, 6], lex)  # the reference's predicate on the touch pair
+    assert st[reps:, 6].min() == 1.0  # left-pad states: the flag is set
+    flags = [st[:, 6].copy()]
+    hold = st.copy()
+    for t in range(30):
+        row = hold.copy()
+        row[:, 6] = min(1.0, 0.5 + t / 30.0)  # gripper command ramping closed, pose held
+        ob.step(row)
+        gb.step(torch.from_numpy(row))
+        torch.cuda.synchronize()
+        g = task_space_state(gb).cpu().numpy()
+        np.testing.assert_array_equal(g, ob.task_space_state(tl, tr), err_msg=f"traj_true row {t}")
+        flags.append(g[:, 6].copy())
+    f = np.stack(flags)
+    assert np.isin(f, (0.0, 1.0)).all()
+    assert (f == 1.0).sum() >= n and (f == 0.0).sum() > 0, f.sum(axis=0)
+    gb.close()

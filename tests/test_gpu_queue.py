@@ -3,6 +3,10 @@
 - Two handles on two streams step 4,096 envs each concurrently (the two queue launches share the
   GPU's workgroup slots, so static first units can belong to workgroups that are not resident): the
   results equal the same handles stepped one after the other, and no unit gives up.
+- The same with most workgroup slots held by a third stream (ur3e_debug_hold_slots: 64 KB-LDS
+  workgroups that stay resident for a few ms, launched and waited for until they all run), so that the
+  queue launches find only one slot per CU: workgroups whose static units are not resident yet, and the
+  consumers claim them.  Claims must happen, nothing gives up, and results equal the sequential runs.
 - Owners that leave their static units to the consumers (diagnostic): every static unit is claimed
   and run by its substep-1 unit, bit-exact against the oracle.
 - A diagnostic spin limit of a few polls forces the give-up path: the envs go to the fallback tiers,
@@ -80,6 +84,54 @@ def test_two_handles_two_streams_concurrent():
         assert giveups == 0, f"handle {h}: {giveups} queue units gave up"
         print(f"handle {h}: static units claimed by consumers: {claimed}")
         bs[h].close()
+
+
+def test_queue_with_slots_held_claims_static_units():
+    torch = _torch()
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model("main")
+    n, steps = 4096, 12
+    cfgs = [rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=s, max_episode_steps=30)
+            for s in (13, 14)]
+    gen = torch.Generator(device="cuda").manual_seed(17)
+    lo = torch.tensor(LO, device="cuda")
+    hi = torch.tensor(HI, device="cuda")
+    acts = [[lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda", generator=gen)
+             for _ in range(steps)] for _ in range(2)]
+    seq = []
+    for h in range(2):
+        b = rt.Batch(mc, cfgs[h], n)
+        for t in range(steps):
+            b.step(acts[h][t])
+        torch.cuda.synchronize()
+        seq.append(_snap(b))
+        b.close()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    holder = torch.cuda.Stream()
+    bs = [rt.Batch(mc, cfgs[h], n) for h in range(2)]
+    torch.cuda.synchronize()
+    props = torch.cuda.get_device_properties(0)
+    n_hold = 2 * props.multi_processor_count  # two 64 KB workgroups per CU
+    started = []
+    for t in range(steps):
+        # slots held before every other step's launches (the hold outlasts a launch: 3 ms)
+        if t % 2 == 0:
+            started.append(rt.hold_slots(n_hold, 3000, stream=holder))
+        for h in range(2):
+            with torch.cuda.stream(streams[h]):
+                bs[h].step(acts[h][t])
+    torch.cuda.synchronize()
+    print(f"hold workgroups started before the launches: {started} of {n_hold}")
+    assert max(started) >= n_hold // 2
+    claimed_total = 0
+    for h in range(2):
+        _cmp(torch, _snap(bs[h]), seq[h], f"handle {h}")
+        giveups, claimed = bs[h].queue_stats()
+        assert giveups == 0, f"handle {h}: {giveups} queue units gave up"
+        print(f"handle {h}: static units claimed by consumers: {claimed}")
+        claimed_total += claimed
+        bs[h].close()
+    assert claimed_total > 0, "the held slots never left a static unit to its consumer"
 
 
 @pytest.mark.parametrize("mode", ["leave_static", "spin_limit"])

@@ -85,9 +85,39 @@ def test_nonconvex_legacy_overcounts():
     exact = M.mesh_inertia(v, f, "exact")[0]
     np.testing.assert_allclose(exact, 3 * 0.01 ** 3, rtol=1e-12)       # three unit squares x 1 cm
     assert M.mesh_inertia(v, f, "convex")[0] > exact                     # the hull fills the notch
-    # legacy sums |tetrahedra| from the vertex centroid: never less than the signed sum (here every
-    # centroid tetrahedron is positive, so it equals it)
+    # legacy sums |tetrahedra| from the surface centroid: never less than the signed sum
     assert M.mesh_inertia(v, f, "legacy")[0] >= exact * (1 - 1e-12)
+
+
+def test_legacy_reference_point_is_the_surface_centroid():
+    """A mesh whose legacy volume depends on the reference point: a thin L prism whose long arm carries
+    most of the surface.  The vertex mean and the surface centroid lie in different places, some
+    tetrahedra change orientation between them, and the legacy volume is the sum of |tetrahedra| from
+    the area-weighted face centroid (MuJoCo's legacy reference; parity vs MuJoCo unpinned), restated
+    here with plain loops."""
+    # L in the xy plane (long arm along x), extruded by h in z; non-convex at the notch
+    P = [(0, 0), (10, 0), (10, 1), (1, 1), (1, 6), (0, 6)]
+    h = 1.0
+    v = np.array([(x, y, 0.0) for x, y in P] + [(x, y, h) for x, y in P])
+    n = len(P)
+    faces = []
+    for i in range(n):  # side quads, outward for a counter-clockwise outline
+        j = (i + 1) % n
+        faces += [(i, j, n + j), (i, n + j, n + i)]
+    for tri in ((0, 2, 1), (0, 3, 2), (0, 4, 3), (0, 5, 4)):  # bottom (fan from vertex 0), facing -z
+        faces.append(tri)
+        faces.append((n + tri[0], n + tri[2], n + tri[1]))  # top, facing +z
+    f = np.array(faces)
+    V_exact = M.mesh_inertia(v, f, "exact")[0]
+    np.testing.assert_allclose(V_exact, (10 * 1 + 1 * 5) * h, rtol=1e-12)
+    area, cen = [], []
+    for a, b, c in f:
+        area.append(0.5 * np.linalg.norm(np.cross(v[b] - v[a], v[c] - v[a])))
+        cen.append((v[a] + v[b] + v[c]) / 3)
+    ref = sum(A * C for A, C in zip(area, cen)) / sum(area)
+    vol_from = lambda r: sum(abs(np.dot(v[a] - r, np.cross(v[b] - r, v[c] - r))) / 6 for a, b, c in f)
+    assert abs(vol_from(ref) - vol_from(v.mean(axis=0))) > 1e-3  # the point matters for this mesh
+    np.testing.assert_allclose(M.mesh_inertia(v, f, "legacy")[0], vol_from(ref), rtol=1e-12)
 
 
 def _model(name):

@@ -3,9 +3,9 @@
 Runs the flop-counting build of the CPU oracle (oracle/flops: the same C sources with `double` ->
 a counting type; +, -, *, / and sqrt each count one) single-threaded on a sample of the bench
 workload -- gym ur3e-v2 on main.xml, frame_skip 2, uniform random actions in the v2 Box, 'high'
-reset noise -- and writes profiles/flops_r01.json.  The GPU kernels execute the same operations in
+reset noise -- and writes profiles/flops_rNN.json (NN: the round, default 04) with the commit it counted.  The GPU kernels execute the same operations in
 the same order (bit-exact parity), so this is also the kernel's algorithmic FP64 work.
-usage: python tools/count_flops.py [n_envs] [steps]"""
+usage: python tools/count_flops.py [n_envs] [steps] [round]"""
 import ctypes
 import json
 import os
@@ -19,7 +19,7 @@ sys.path.insert(0, REPO)
 os.environ["OMP_NUM_THREADS"] = "1"
 
 
-def main(n=64, steps=100, out_path=None):
+def main(n=64, steps=100, rnd=4, out_path=None):
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "flops"], check=True, stdout=subprocess.DEVNULL)
@@ -47,11 +47,13 @@ def main(n=64, steps=100, out_path=None):
                      f"'high' reset noise)",
            "counted": "FP64 +, -, *, /, sqrt in the oracle's pipeline (controller, 2 x mj_step, obs/reward); "
                       "comparisons, selects, fabs not counted",
-           "source": "tools/count_flops.py over oracle/flops (counting build of oracle/)"}
-    with open(out_path or os.path.join(REPO, "profiles", "flops_r01.json"), "w") as f:
+           "source": "tools/count_flops.py over oracle/flops (counting build of oracle/)",
+           "head": subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                  text=True).stdout.strip() or None}
+    with open(out_path or os.path.join(REPO, "profiles", f"flops_r{rnd:02d}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(*(int(x) for x in sys.argv[1:3]))
+    main(*(int(x) for x in sys.argv[1:4]))

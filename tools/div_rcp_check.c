@@ -1,7 +1,8 @@
 /* Host check of k_div_rcp (ur3e_amd/csrc/ur3e_engine.h): with r = 1.0 / d and q0 = n * r,
    fma(-fma(d, q0, -n), r, q0) == n / d bit for bit (signed zeros included), d > 0.
    Operands: random across 120 binades of n and 60 of d (signed zeros every 17th pair), then
-   structured pairs (integers, d near 1 and near powers of two, quotients near representable values).
+   structured pairs (integers, d near 1 and near powers of two, quotients near representable values),
+   then the numerator extremes the guard sends to a true division (subnormal, tiny, huge, infinite).
    gcc -O2 -ffp-contract=off tools/div_rcp_check.c -lm -o /tmp/drc && /tmp/drc [pairs]
    (tests/test_div_rcp.py builds and runs it with a smaller count; the round-3 run used 4e8 + 2e8). */
 #include <math.h>
@@ -27,8 +28,14 @@ static double rnd(int emin, int emax) {
   return d;
 }
 static long bad = 0;
+/* k_div_rcp as ur3e_engine.h defines it (the guard included) */
+static double div_rcp(double n, double d, double r) {
+  double q0 = n * r, e = fma(d, q0, -n), q = fma(-e, r, q0), an = fabs(n);
+  if (an > 0.0 && (an < 0x1p-960 || an > 0x1p+960)) q = n / d;
+  return q;
+}
 static void check(double a, double d) {
-  double r = 1.0 / d, q0 = a * r, e = fma(d, q0, -a), q1 = fma(-e, r, q0), ref = a / d;
+  double r = 1.0 / d, q1 = div_rcp(a, d, r), ref = a / d;
   if (memcmp(&q1, &ref, 8)) {
     if (bad < 10) printf("a=%a d=%a ref=%a got=%a\n", a, d, ref, q1);
     bad++;
@@ -63,6 +70,23 @@ int main(int argc, char** argv) {
     }
     check(a, d);
   }
-  printf("pairs=%ld bad=%ld\n", n + n / 2, bad);
+  /* the numerator extremes: subnormal, tiny (binades -1074..-850), huge (900..1023) and infinite, with
+     divisors over the callers' range (2^-50: norms >= mjMINVAL = 1e-15; up to 2^40: Cholesky pivots) */
+  for (long i = 0; i < n / 2; i++) {
+    double a, d = ldexp(1.0 + ldexp((double)(xr() >> 12), -52), -50 + (int)(xr() % 91));
+    uint64_t b;
+    switch (i % 4) {
+      case 0:
+        b = xr() & ((1ull << 52) - 1);
+        if (xr() & 1) b |= 1ull << 63;
+        memcpy(&a, &b, 8);
+        break;
+      case 1: a = rnd(-1022, -850); break;
+      case 2: a = rnd(900, 1023); if (fabs(a) / d > 1.7e308) a = ldexp(a, -60); break;
+      default: a = (xr() & 1) ? INFINITY : -INFINITY; break;
+    }
+    check(a, d);
+  }
+  printf("pairs=%ld bad=%ld\n", n + n, bad);
   return bad != 0;
 }

@@ -6,7 +6,7 @@ coalesced read, so the fetch figure is doubled.  usage: summarize_profile.py gpu
 import csv, json, os, shutil, sys
 
 src, name = sys.argv[1], sys.argv[2]
-rnd = sys.argv[3] if len(sys.argv) > 3 else "r02"
+rnd = sys.argv[3] if len(sys.argv) > 3 else "r04"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(REPO, "profiles", name)
 os.makedirs(dst, exist_ok=True)
@@ -62,7 +62,12 @@ if os.path.exists(sq2p):
         sq2["valu_lane_utilisation"] = sq2["SQ_THREAD_CYCLES_VALU"] / (4.0 * sq2["SQ_ACTIVE_INST_VALU"] * 64.0)
     sqs.update({k: v for k, v in sq2.items() if k != "SQ_WAVES"})
 json.dump(sqs, open(os.path.join(dst, "pmc_sq.json"), "w"), indent=1)
-json.dump({"hbm_bytes_per_launch": hbm["hbm_bytes_per_launch"], "source": f"profiles/{name}/pmc_hbm.json"},
+import subprocess
+head = subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+dirty = subprocess.run(["git", "-C", REPO, "status", "--porcelain", "--untracked-files=no", "--", "ur3e_amd/csrc",
+                        "include"], capture_output=True, text=True).stdout.strip()
+json.dump({"hbm_bytes_per_launch": hbm["hbm_bytes_per_launch"], "source": f"profiles/{name}/pmc_hbm.json",
+           "head": head + ("+dirty-csrc" if dirty else ""), "kernel": hbm["kernel"]},
           open(os.path.join(REPO, "profiles", f"traffic_{rnd}.json"), "w"))
 stats = list(csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))))
 for r in stats[:4]:

@@ -32,7 +32,8 @@ def task_space_state(batch, out=None):
     on the device (ur3e_batch_get_task_space_state); `out` may be a row of a recording buffer."""
     if out is None:
         return batch.get_task_space_state()
-    batch._chk(batch.L.ur3e_batch_get_task_space_state(batch.h, batch.torch_ptr(out), batch._stream()))
+    batch._chk(batch.L.ur3e_batch_get_task_space_state(batch.h, batch.out_ptr(out, 7, "task_space_state"),
+                                                       batch._stream()))
     return out
 
 

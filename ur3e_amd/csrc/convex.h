@@ -318,7 +318,13 @@ typedef struct {
   int nf;
 } ur3e_epa;
 
-UR3E_HD int ur3e_epa_face(ur3e_epa* P, int i, int j, int k) {
+/* add face (i, j, k).  orient = 1 (the initial tetrahedron, whose winding is arbitrary): wind it so that
+   its normal points away from the origin, which lies inside.  orient = 0 (a horizon face (i, j, new
+   vertex), with the edge (i, j) in the winding of the removed face it bordered): the winding is already
+   outward, so the normal follows it and the plane offset keeps its sign -- when the origin lies on or
+   within rounding of the face plane (touching and shallow contacts), a sign test could flip the normal
+   inward and reverse the contact normal. */
+UR3E_HD int ur3e_epa_face(ur3e_epa* P, int i, int j, int k, int orient) {
   if (P->nf >= UR3E_EPA_MAXF) return -1;
   double ab[3], ac[3], n[3];
   ur3e_cvx_sub(ab, P->w[j], P->w[i]);
@@ -329,7 +335,7 @@ UR3E_HD int ur3e_epa_face(ur3e_epa* P, int i, int j, int k) {
   n[0] /= len; n[1] /= len; n[2] /= len;
   double d = ur3e_cvx_dot(n, P->w[i]);
   int f = P->nf++;
-  if (d < 0) { /* orient outward (the origin is inside the polytope) */
+  if (orient && d < 0) {
     P->f[f][0] = i; P->f[f][1] = k; P->f[f][2] = j;
     n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2];
     d = -d;
@@ -386,8 +392,8 @@ UR3E_HD int ur3e_epa_run(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, 
   if (s->n < 4 && !ur3e_epa_seed(A, B, s)) return 0;
   P->nv = 0; P->nf = 0;
   for (int k = 0; k < 4; k++) ur3e_epa_addv(P, s->w[k], s->a[k], s->b[k]);
-  if (ur3e_epa_face(P, 0, 1, 2) < 0 || ur3e_epa_face(P, 0, 3, 1) < 0 || ur3e_epa_face(P, 0, 2, 3) < 0 ||
-      ur3e_epa_face(P, 1, 3, 2) < 0)
+  if (ur3e_epa_face(P, 0, 1, 2, 1) < 0 || ur3e_epa_face(P, 0, 3, 1, 1) < 0 || ur3e_epa_face(P, 0, 2, 3, 1) < 0 ||
+      ur3e_epa_face(P, 1, 3, 2, 1) < 0)
     return 0;
   int best = 0;
   for (int it = 0; it < UR3E_EPA_ITERS; it++) {
@@ -425,7 +431,7 @@ UR3E_HD int ur3e_epa_run(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, 
     }
     int ok = 1;
     for (int q = 0; q < ne; q++)
-      if (ur3e_epa_face(P, edges[q][0], edges[q][1], nvx) < 0) ok = 0;
+      if (ur3e_epa_face(P, edges[q][0], edges[q][1], nvx, 0) < 0) ok = 0;
     if (!ok) break;
   }
   /* contact from the closest face: the origin's projection in barycentric coordinates */

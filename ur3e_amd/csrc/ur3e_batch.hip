@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <chrono>
 
 #include "../../include/ur3e_batch.h"
 #include "ur3e_engine.h"
@@ -2421,6 +2422,62 @@ extern "C" int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_lim
   if (!b) return fail(UR3E_EINVAL, "null handle");
   b->cfg.spin_limit = spin_limit;
   b->cfg.leave_static = leave_static_units != 0;
+  return UR3E_OK;
+}
+
+/* Diagnostic for the queue's forward-progress test: workgroups that each hold 64 KB of LDS (two per CU
+   fill 128 of the 160 KB, leaving room for one step workgroup) for hold_us microseconds of the constant
+   100 MHz clock from their own start, then exit -- every wave reaches the exit.  Each sets its flag in
+   host-mapped memory when it starts, so the host can wait until they are all resident before it
+   launches the queue on another stream. */
+#define W_HOLD_LDS_DOUBLES 8192
+__global__ __launch_bounds__(64) void w_hold_slots(unsigned int* started, unsigned long long ticks, double* sink) {
+  __shared__ double buf[W_HOLD_LDS_DOUBLES];
+  const int l = threadIdx.x;
+  for (int i = l; i < W_HOLD_LDS_DOUBLES; i += 64) buf[i] = (double)i;
+  __syncthreads();
+  /* a plain store per workgroup into host-mapped memory (no PCIe atomics needed) */
+  if (l == 0) __hip_atomic_store(started + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long t0 = wall_clock64();
+  double acc = 0.0;
+  int k = l;
+  while (wall_clock64() - t0 < ticks) {
+    acc += buf[k];
+    k = (k + 64) & (W_HOLD_LDS_DOUBLES - 1);
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (acc == -1.0) sink[l] = acc; /* never true: keeps the LDS reads */
+}
+
+extern "C" int ur3e_debug_hold_slots(int device, int workgroups, int hold_us, void* stream, int* started) {
+  if (workgroups <= 0 || workgroups > 4096 || hold_us <= 0 || hold_us > 1000000)
+    return fail(UR3E_EINVAL, "workgroups in [1, 4096], hold_us in [1, 1e6]");
+  HIPCHK(hipSetDevice(device));
+  /* one host-mapped counter and sink per process, kept for its lifetime: the call returns while the
+     workgroups still hold their slots.  The counter is re-zeroed only after every workgroup of the
+     previous call had started (they count only at their start). */
+  static unsigned int* cnt = nullptr; /* one start flag per workgroup */
+  static unsigned int* dcnt = nullptr;
+  static double* sink = nullptr;
+  if (!cnt) {
+    HIPCHK(hipHostMalloc((void**)&cnt, 4096 * sizeof(unsigned int), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&dcnt, cnt, 0));
+    HIPCHK(hipMalloc((void**)&sink, 64 * sizeof(double)));
+  }
+  for (int i = 0; i < workgroups; i++) ((volatile unsigned int*)cnt)[i] = 0;
+  const unsigned long long ticks = 100ull * (unsigned long long)hold_us; /* wall_clock64: 100 MHz */
+  hipLaunchKernelGGL(w_hold_slots, dim3(workgroups), dim3(64), 0, (hipStream_t)stream, dcnt, ticks, sink);
+  HIPCHK(hipGetLastError());
+  /* wait (bounded by twice the hold time) until every workgroup has started, then return: the caller
+     launches the work that is to find its slots taken */
+  const auto t0 = std::chrono::steady_clock::now();
+  int seen = 0;
+  for (;;) {
+    seen = 0;
+    for (int i = 0; i < workgroups; i++) seen += ((volatile unsigned int*)cnt)[i] != 0;
+    if (seen >= workgroups || std::chrono::steady_clock::now() - t0 >= std::chrono::microseconds(2 * hold_us)) break;
+  }
+  if (started) *started = seen;
   return UR3E_OK;
 }
 

@@ -62,12 +62,22 @@
    quotient (Markstein's theorem: r within half an ulp of 1/d, q0 within an ulp of n/d; no underflow or
    overflow).  Signed zeros: n = -0 gives q0 = -0, e = +0, -0 - (+0) r = -0, as -0 / d.  Three
    operations instead of the ~11 of a full division, so several quotients by one divisor cost one
-   division and three operations each.  tools/div_rcp_check.c checks it against n / d over 6e8 random
-   and structured operand pairs (tests/test_div_rcp.py). */
+   division and three operations each.  The theorem needs the residual to stay out of the subnormal
+   range: with |n| below 2^-960 (subnormal numerators included) it does not hold (the host check finds
+   one-ulp misses there), nor for |n| above 2^960 or infinite, so those numerators -- never seen on the
+   path, but possible -- take the true division behind a branch that no lane normally enters.
+   tools/div_rcp_check.c checks the whole function against n / d over random and structured operand
+   pairs, subnormal, tiny, huge and infinite numerators included, for the divisor ranges the callers
+   use (Cholesky pivots >= sqrt(mjMINVAL), norms >= mjMINVAL; tests/test_div_rcp.py). */
+#define K_RCP_NLO 0x1p-960
+#define K_RCP_NHI 0x1p+960
 KD double k_div_rcp(double n, double d, double r) {
   const double q0 = n * r;
   const double e = __builtin_fma(d, q0, -n);
-  return __builtin_fma(-e, r, q0);
+  double q = __builtin_fma(-e, r, q0);
+  const double an = __builtin_fabs(n);
+  if (__builtin_expect(an > 0.0 && (an < K_RCP_NLO || an > K_RCP_NHI), 0)) q = n / d;
+  return q;
 }
 /* this lane's index within the workgroup, opaque to the optimiser: a value derived from
    threadIdx.x alone is loop-invariant, and LICM would hoist all of them out of the per-substep

@@ -196,7 +196,7 @@ def _tet_props(a, b, c):
 def mesh_inertia(v, f, mode: str = "legacy"):
     """(volume, com [3], inertia tensor about the com [3, 3]) of the solid bounded by triangles f over v
     (unit density).  mode: 'exact' (signed tetrahedra from the origin), 'convex' (the same over the convex
-    hull), 'legacy' (tetrahedra from the vertex centroid, absolute volumes), 'shell' (unit surface
+    hull), 'legacy' (tetrahedra from the area-weighted surface centroid, absolute volumes), 'shell' (unit surface
     density: triangle areas at their centroids with the thin-triangle second moments)."""
     v = np.asarray(v, dtype=np.float64)
     f = np.asarray(f, dtype=np.int64)
@@ -215,7 +215,15 @@ def mesh_inertia(v, f, mode: str = "legacy"):
             cov += area[k] / 12.0 * (np.outer(a[k], a[k]) + np.outer(b[k], b[k]) + np.outer(c[k], c[k]) +
                                      np.outer(s[k], s[k]))
         return A, com, np.trace(cov) * np.eye(3) - cov
-    ref = v.mean(axis=0) if mode == "legacy" else np.zeros(3)
+    if mode == "legacy":
+        # MuJoCo's legacy volume: tetrahedra from the surface centroid (face centroids weighted by face
+        # area), absolute volumes.  For a convex or star-shaped mesh any interior point gives the same
+        # sum; for a non-convex one the point matters (parity vs MuJoCo unpinned: its source is absent)
+        a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+        area = 0.5 * np.linalg.norm(np.cross(b - a, c - a), axis=1)
+        ref = (area[:, None] * (a + b + c) / 3.0).sum(0) / area.sum()
+    else:
+        ref = np.zeros(3)
     a, b, c = v[f[:, 0]] - ref, v[f[:, 1]] - ref, v[f[:, 2]] - ref
     vol, cen, cov = _tet_props(a, b, c)
     if mode == "legacy":

@@ -94,11 +94,24 @@ def _bind(L):
     L.ur3e_batch_get_actuator_force.argtypes = [vp, vp, vp]
     L.ur3e_batch_queue_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_set_queue_debug.argtypes = [vp, ctypes.c_uint, ip]
+    L.ur3e_debug_hold_slots.argtypes = [ip, ip, ip, vp, ctypes.POINTER(ip)]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim",
               "ur3e_batch_schedule"):
         getattr(L, f).argtypes = [vp]
     del dp
     return L
+
+
+def hold_slots(workgroups: int, hold_us: int, stream=None, device: int = 0) -> int:
+    """Diagnostic: occupy most workgroup slots of the GPU for hold_us microseconds (ur3e_debug_hold_slots)
+    on `stream` (a torch stream; default: torch's current stream); returns once they are all resident,
+    with the number that had started."""
+    import torch
+    L = load_library()
+    st = (stream or torch.cuda.current_stream(device)).cuda_stream
+    started = ctypes.c_int()
+    _check(L.ur3e_debug_hold_slots(device, workgroups, hold_us, ctypes.c_void_p(st), ctypes.byref(started)), L)
+    return started.value
 
 
 def _check(rc, L=None):
@@ -116,7 +129,7 @@ def load_model(name: str = "main"):
 def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_reset=True, reset_noise=True,
                 reset_key=None, model=None, seed=0, env_id_offset=0, envs_per_block=0,
                 task_gains=None, joint_gains=None, tier_con_cap=0, rot_joint_gains=None,
-                np_chunk_lanes=0, sensors=False, schedule=0) -> ConfigC:
+                np_chunk_lanes=0, sensors=False, schedule=0, config_yaml_path=None) -> ConfigC:
     c = ConfigC()
     c.task = task
     c.frame_skip = frame_skip
@@ -130,6 +143,16 @@ def make_config(task=TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, auto_res
     c.reset_key = reset_key
     tg = task_gains or GAINS_L_MUG
     g = list(tg["kp_pos"]) + list(tg["kd_pos"]) + list(tg["kp_rot"]) + list(tg["kd_rot"])
+    if (joint_gains is None or rot_joint_gains is None) and task in (TASK_MOVE_J, TASK_MOVE_L):
+        # the reference's drivers read their gains from the YAML configs (move_j.py:46-52: config_j.yml;
+        # move_l.py:92-99: config_l.yml, pos and rot sections), from the cwd as it does, else the packaged copies
+        from . import gains as _gains
+        if task == TASK_MOVE_J:
+            joint_gains = joint_gains or _gains.joint_gains(config_yaml_path)
+        else:
+            mpos, mrot = _gains.move_l_gains(config_yaml_path)
+            joint_gains = joint_gains or mpos
+            rot_joint_gains = rot_joint_gains or mrot
     jg = joint_gains or (GAINS_L_POS if task == TASK_MOVE_L else GAINS_J)
     j = list(jg["kp"]) + list(jg["kd"])
     rg = rot_joint_gains or GAINS_L_ROT
@@ -192,8 +215,26 @@ class Batch:
     @staticmethod
     def torch_ptr(t):
         """device pointer of a contiguous tensor (or a contiguous row view of one)"""
-        assert t.is_contiguous()
+        if not t.is_contiguous():
+            raise ValueError("ur3e_amd: tensor must be contiguous")
         return _ptr(t)
+
+    def out_ptr(self, out, cols: int, what: str):
+        """device pointer of a caller-provided output buffer the kernels fill with n x cols doubles:
+        checked for device, dtype, shape and contiguity before any launch (a wrong buffer would be
+        written out of bounds on the device)"""
+        t = self.torch
+        if not isinstance(out, t.Tensor):
+            raise ValueError(f"{what}: out must be a torch tensor")
+        if out.device != self.device:
+            raise ValueError(f"{what}: out is on {out.device}, the batch on {self.device}")
+        if out.dtype != t.float64:
+            raise ValueError(f"{what}: out must be float64, got {out.dtype}")
+        if tuple(out.shape) != (self.n, cols):
+            raise ValueError(f"{what}: out must have shape ({self.n}, {cols}), got {tuple(out.shape)}")
+        if not out.is_contiguous():
+            raise ValueError(f"{what}: out must be contiguous")
+        return _ptr(out)
 
     def _chk(self, rc):
         _check(rc, self.L)
@@ -276,7 +317,8 @@ class Batch:
         of a recording buffer"""
         if out is None:
             out = self.torch.empty((self.n, self.nu), dtype=self.torch.float64, device=self.device)
-        self._chk(self.L.ur3e_batch_get_actuator_force(self.h, _ptr(out), self._stream()))
+        self._chk(self.L.ur3e_batch_get_actuator_force(self.h, self.out_ptr(out, self.nu, "get_actuator_force"),
+                                                       self._stream()))
         return out
 
     def get_carry(self):
