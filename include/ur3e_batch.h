@@ -36,6 +36,8 @@
  *                       MjData.qpos/qvel/qacc_warmstart read/write + mj_forward
  *                       (MujocoEnv.set_state; utils/utils.py:15-24)
  *   ur3e_batch_destroy  env.close()
+ *   ur3e_batch_create_from_mjcf
+ *                       gymnasium.make / init_mj.py:22-30 from the model file and gain YAML
  */
 #ifndef UR3E_BATCH_H
 #define UR3E_BATCH_H
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 7
+#define UR3E_ABI_VERSION 8
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -117,6 +119,23 @@ typedef struct ur3e_batch ur3e_batch_t;
 
 int ur3e_abi_version(void);
 const char* ur3e_last_error(void);
+
+/* The reference's files as the model and gains (ur3e_amd/csrc/ur3e_mjcf.cpp), for callers that are not
+   Python.  The MJCF compiler and the YAML reader are the package's Python (ur3e_amd/model/compiler.py,
+   ur3e_amd/gains.py), run through an embedded interpreter (libpython loaded on first use; in a Python
+   process, the running one); nothing here touches the GPU.
+     ur3e_model_from_mjcf: compile an MJCF file (assets/main.xml, ur3e_2f85.xml, ur3e_raw.xml: what
+       MujocoEnv.__init__ / init_mj.py:22-30 load) into *out; meshes = "auto" (NULL), "mesh" or
+       "surrogate" (ur3e_amd/model/compiler.py: real convex meshes when the files exist, else boxes).
+     ur3e_config_gains_from_yaml: fill cfg's gains for cfg->task from a gain file as the reference reads
+       it (task-space tasks: config_l_mug.yml, ur3e_env2.py:66-68; move_j: config_j.yml, move_j.py:46-52;
+       move_l: config_l.yml, move_l.py:92-99); NULL: controller/config/<file> under the working
+       directory, else the packaged copy of the reference's values.
+     ur3e_batch_create_from_mjcf: both, then ur3e_batch_create (cfg's gains are replaced). */
+int ur3e_model_from_mjcf(const char* mjcf_path, const char* meshes, ur3e_model_t* out);
+int ur3e_config_gains_from_yaml(const char* config_yaml_path, ur3e_config_t* cfg);
+int ur3e_batch_create_from_mjcf(const char* mjcf_path, const char* config_yaml_path, const ur3e_config_t* cfg,
+                                int n_envs, int device, ur3e_batch_t** out);
 
 /* allocates N envs at qpos0 / zero velocity; like gymnasium, call ur3e_batch_reset before stepping */
 int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,
