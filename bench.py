@@ -148,7 +148,7 @@ def cpu_other_configs(L, threads, c2_envs=4096, c2_steps=200, c3_envs=1024, c3_r
 
 
 def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_core_steps=400,
-                 all_cores_steps=300):
+                 all_cores_steps=100):
     """The cpu_baseline leg.  The oracle (oracle/, the same algorithm in C) is compiled for this host
     (-O3 -march=native -ffp-contract=off, OpenMP over envs) and timed on a bounded sample of the bench
     workload: (1) this process's CPU share (OMP_NUM_THREADS, 16 per GPU on the box): n_envs_sample gym

@@ -1,4 +1,4 @@
-"""k_normalize4's decisions on the squared norm (tools/var/nrm4sq.patch to ur3e_amd/csrc/ur3e_engine.h) equal the oracle's
+"""k_normalize4's decisions on the squared norm (ur3e_amd/csrc/ur3e_engine.h) equal the oracle's
 decisions on the norm (mju_normalize4): the constants match tools/normalize_thresholds.py and the two
 tests agree on every double within 1e5 ulps of each boundary and on random squared norms."""
 import math
@@ -12,8 +12,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import normalize_thresholds as nt  # noqa: E402
 
 
-def test_constants_match_patch():
-    src = open(os.path.join(ROOT, "tools", "var", "nrm4sq.patch")).read()
+def test_constants_match_the_kernel_source():
+    src = open(os.path.join(ROOT, "ur3e_amd", "csrc", "ur3e_engine.h")).read()
     for k, v in nt.thresholds().items():
         m = re.search(r"#define %s (\S+)" % k, src)
         assert m, k

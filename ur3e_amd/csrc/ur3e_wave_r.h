@@ -628,13 +628,30 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   /* forward: L y = grad (x[k] = tmp[k] / L[k][k]; tmp[i] -= L[i][k] x[k], i > k).  Every lane applies
      the update (no lane > k select): lane k keeps its result in yf, and the lanes < k, already final in
      yf, only disturb their dead tmp (their h[k] is the unread upper triangle) */
-  double tmp = grad, yf = 0.0;
+  /* Every lane runs the three operations, but only lane k's quotient is used: the dead lanes' tmp is
+     arbitrary, so the numerator check of k_div_rcp would send them to its true division at random.
+     Lane k keeps its own numerator (nf), checked once after the sweep; the rare sweep whose used
+     numerators left Markstein's range is redone with the true divisions (uniform, same bits). */
+  double tmp = grad, yf = 0.0, nf = 0.0;
 #pragma unroll
   for (int k = 0; k < K_NV; k++) {
     if (k < nv) {
-      double xk = rl(k_div_rcp(tmp, dg, rdg), k);
+      double xk = rl(k_div_rcp_raw(tmp, dg, rdg), k);
       yf = lane == k ? xk : yf;
+      nf = lane == k ? tmp : nf;
       tmp -= h[k] * xk;
+    }
+  }
+  if (__builtin_expect(w_any<64>(lane < nv && k_rcp_unsafe(nf)), 0)) {
+    tmp = grad;
+    yf = 0.0;
+#pragma unroll
+    for (int k = 0; k < K_NV; k++) {
+      if (k < nv) {
+        const double xk = rl(tmp, k) / rl(dg, k);
+        yf = lane == k ? xk : yf;
+        tmp -= h[k] * xk;
+      }
     }
   }
   WT(18);
@@ -647,12 +664,26 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
      every lane updates and lane i keeps x[i] in xf (the lanes > i are final) */
   tmp = yf;
   double xf = 0.0;
+  nf = 0.0;
 #pragma unroll
   for (int i = K_NV - 1; i >= 0; i--) {
     if (i < nv) {
-      double xi = rl(k_div_rcp(tmp, dg, rdg), i); /* lane i: lt[i] = L[i][i] = dg */
+      double xi = rl(k_div_rcp_raw(tmp, dg, rdg), i); /* lane i: lt[i] = L[i][i] = dg */
       xf = lane == i ? xi : xf;
+      nf = lane == i ? tmp : nf;
       tmp -= lt[i] * xi;
+    }
+  }
+  if (__builtin_expect(w_any<64>(lane < nv && k_rcp_unsafe(nf)), 0)) {
+    tmp = yf;
+    xf = 0.0;
+#pragma unroll
+    for (int i = K_NV - 1; i >= 0; i--) {
+      if (i < nv) {
+        const double xi = rl(tmp, i) / rl(dg, i);
+        xf = lane == i ? xi : xf;
+        tmp -= lt[i] * xi;
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();

@@ -153,11 +153,14 @@ def _attrs(defaults, el, childclass):
 
 
 # ---------------------------------------------------------------------------
-def _mesh_assets(root, defaults, path):
-    """<asset><mesh> entries: name -> {file (resolved against <compiler meshdir>), scale, inertia}"""
+def _mesh_assets(root, defaults, path, meshdir_override=None):
+    """<asset><mesh> entries: name -> {file (resolved against <compiler meshdir>, or against
+    meshdir_override when given), scale, inertia}"""
     comp = root.find("compiler")
     meshdir = comp.get("meshdir", "") if comp is not None else ""
     base = os.path.join(os.path.dirname(os.path.abspath(path)), meshdir)
+    if meshdir_override is not None:
+        base = meshdir_override
     out = {}
     asset = root.find("asset")
     if asset is None:
@@ -174,16 +177,18 @@ def _mesh_assets(root, defaults, path):
     return out
 
 
-def compile_mjcf(path: str, meshes: str = "auto") -> dict:
+def compile_mjcf(path: str, meshes: str = "auto", meshdir: str | None = None) -> dict:
     """Compile one MJCF file into a model dict.  meshes: "auto" = real mesh geoms when every mesh file
-    exists, else the box surrogate; "mesh" = real meshes (missing files raise); "surrogate"."""
+    exists, else the box surrogate; "mesh" = real meshes (missing files raise); "surrogate".
+    meshdir: resolve the mesh files against this directory instead of the MJCF's <compiler meshdir>
+    (the same relative file names), e.g. a directory of substitute meshes."""
     tree = ET.parse(path)
     root = tree.getroot()
     defaults = _Defaults(root)
     model_name = os.path.basename(path)
     if meshes not in ("auto", "mesh", "surrogate"):
         raise ValueError(f"meshes must be 'auto', 'mesh' or 'surrogate', got {meshes!r}")
-    assets = _mesh_assets(root, defaults, path)
+    assets = _mesh_assets(root, defaults, path, meshdir)
     missing = [a["file"] for a in assets.values() if not os.path.exists(a["file"])]
     if meshes == "mesh" and missing:
         raise FileNotFoundError(f"mesh files missing: {missing}")
