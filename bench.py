@@ -265,6 +265,28 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
     out["C2_ur3e_2f85_move_j"] = {"value": timed(lambda: b.step(next(it))), "unit": "env-steps/s",
                                   "envs": n_envs, "substeps_per_env_step": 1}
     b.close()
+    # the headline workload on main.xml with convex meshes (synthetic stand-in hulls for the mesh files the
+    # reference does not ship, tools/make_main_meshes.py): the mesh-capable tier set, GJK in the compact tier
+    md_m, mc_m = rt.load_model("main_mesh")
+    cfg_m = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md_m, seed=1234)
+    bm = rt.Batch(mc_m, cfg_m, n_envs)
+    lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
+    hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
+    acts_m = lo + (hi - lo) * torch.rand((200 + warmup + steps, n_envs, 4), dtype=torch.float64, device=dev,
+                                         generator=g)
+    for t in range(200):  # mid-episode, as the headline window
+        bm.step(acts_m[t])
+    tc0 = bm.tier_counts()
+    it = iter(acts_m[200:])
+    val = timed(lambda: bm.step(next(it)))
+    tc = [x - y for x, y in zip(bm.tier_counts(), tc0)]
+    tot = float(n_envs * (warmup + steps))
+    out["main_mesh_gym_v2"] = {"value": val, "unit": "env-steps/s", "envs": n_envs, "substeps_per_env_step": 2,
+                               "model": "main.xml with convex meshes (24 colliding geoms, 17 meshes, 234 pairs)",
+                               "kernel_resources": bm.kernel_info(),
+                               "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
+                               "grasp_tier_routed_frac": tc[2] / tot}
+    bm.close()
     # C3 is timed over the grasp: rows 1500-2600 of build_traj_l_pick_place (build_traj.py:28-59: the
     # descent to the mug ends at row 1800, the gripper closes and the lift starts), reached untimed
     drv = MoveLMug(n_envs, reset_mode="low", seed=0)

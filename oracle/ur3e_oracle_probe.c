@@ -95,3 +95,11 @@ void ur3o_data_rnepost(const ur3e_model_t* m, const ur3o_data* d, double* cacc, 
   memcpy(cfrc_int, d->cfrc_int, sizeof(double) * 6 * m->nbody);
   memcpy(cfrc_ext, d->cfrc_ext, sizeof(double) * 6 * m->nbody);
 }
+
+/* geom poses of the last forward: xpos [ngeom, 3], xmat [ngeom, 9] (tier-routing diagnostics) */
+void ur3o_data_geom_pose(const ur3e_model_t* m, const ur3o_data* d, double* xpos, double* xmat) {
+  for (int g = 0; g < m->ngeom; g++) {
+    memcpy(xpos + 3 * g, d->geom_xpos[g], sizeof(double) * 3);
+    memcpy(xmat + 9 * g, d->geom_xmat[g], sizeof(double) * 9);
+  }
+}

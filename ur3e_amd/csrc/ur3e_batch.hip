@@ -33,7 +33,6 @@
 #include "ur3e_engine.h"
 #include "ur3e_wave.h"
 
-#define NCARRY 54
 
 /* ================================================================== */
 /* scipy Rotation semantics (controller_func.get_rot_err)              */
@@ -399,9 +398,9 @@ struct KState {
   int* routed_host;
 };
 /* an env whose last forward had more contacts or constraint rows than these runs its next step in
-   the grasp tier (the compact tier holds 10 contacts / 44 rows; the margin covers the contacts and
-   joint-limit rows one step can add) */
-#define W_ROUTE_NCON 8
+   the grasp tier (the compact tier holds W_SMALL_MAXCON contacts / W_SMALL_MAXEFC rows; the margin
+   covers a contact or three joint-limit rows one step can add) */
+#define W_ROUTE_NCON (W_SMALL_MAXCON - 1)
 /* host-side routing decision (ur3e_batch_step): run-ahead bound and how long routing stays on after
    the host last saw a routed env */
 #define W_AHEAD 16
@@ -409,7 +408,7 @@ struct KState {
 #define W_ROUTE_HOLD 64
 /* grasp-tier workgroups for the compact tier's bails while routing is off (bails are rare then) */
 #define W_GRASP_IDLE_GRID 128
-#define W_ROUTE_NEFC 36
+#define W_ROUTE_NEFC (W_SMALL_MAXEFC - 3)
 
 struct KConfig {
   int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
@@ -871,7 +870,6 @@ KD void w_task_obs(KModel m, const KS& s, int task, double* obs) {
 struct WOut {
   double obs[24];
   double tobs[24];
-  double carry[NCARRY];
   double a[8];
   double r, ep_return;
   int term, trunc, t, ep_len, did_reset;
@@ -880,6 +878,42 @@ struct WOut {
      commit): kept in a register across the step it and the addresses derived from it were spilled */
   int e;
 };
+
+/* The compact tier's working set (the overlaid layout, with WOut behind it) lives in DYNAMIC LDS, sized
+   at launch (w_dyn_lds): with static LDS the compiler derives the kernel's occupancy from it -- 16 KB
+   allows 10 workgroups per CU, i.e. 2.5 waves per SIMD, which it rounds down to 2 and then keeps 206
+   registers, so no SIMD would take a third wave.  Out of its sight, the kernel is compiled for three
+   waves per SIMD (168 registers, W_COMPACT_WPE) and the hardware places ten envs per CU.  The other
+   layouts keep static LDS. */
+template <class KS>
+constexpr size_t w_wout_off() { return (sizeof(KS) + 15) & ~(size_t)15; }
+/* W_DYN_PAD: diagnostic builds only (A/B of the register budget at a fixed occupancy): extra dynamic
+   LDS per compact workgroup */
+#ifndef W_DYN_PAD
+#define W_DYN_PAD 0
+#endif
+template <class KS>
+constexpr size_t w_dyn_lds() { return KS::OVERLAY ? w_wout_off<KS>() + sizeof(WOut) + W_DYN_PAD : 0; }
+template <class KS>
+__device__ __forceinline__ KS& w_smem() {
+  if constexpr (KS::OVERLAY) {
+    extern __shared__ __align__(16) char w_dyn[];
+    return *reinterpret_cast<KS*>(w_dyn);
+  } else {
+    __shared__ KS s;
+    return s;
+  }
+}
+template <class KS>
+__device__ __forceinline__ WOut& w_wout() {
+  if constexpr (KS::OVERLAY) {
+    extern __shared__ __align__(16) char w_dyn[];
+    return *reinterpret_cast<WOut*>(w_dyn + w_wout_off<KS>());
+  } else {
+    __shared__ WOut o;
+    return o;
+  }
+}
 
 template <int NT, class KS>
 WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut& o) {
@@ -909,7 +943,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   const int tid = w_lane();
   for (int k = tid; k < m->nq; k += NT) st.qpos[SQ(st, k, e)] = s.qpos[k];
   for (int k = tid; k < m->nv; k += NT) { st.qvel[SV(st, k, e)] = s.qvel[k]; st.warm[SV(st, k, e)] = s.warm[k]; }
-  for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = o.carry[k];
+  for (int k = tid; k < NCARRY; k += NT) st.carry[SC(st, k, e)] = s.carry[k];
   for (int k = tid; k < UR3E_MAXTOUCH; k += NT) st.touch[(size_t)e * UR3E_MAXTOUCH + k] = s.touch[k];
   for (int k = tid; k < m->nu; k += NT) {
     st.ctrl[(size_t)e * UR3E_MAXU + k] = s.ctrl[k];
@@ -972,7 +1006,7 @@ WD void w_reset_finish(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   const int TASK = TK >= 0 ? TK : c.task; /* TK >= 0: kernel specialised for one task at compile time */
   const int tid = w_lane();
   if (tid == 0 && (k_is_gym(TASK) || c.obs_sites)) w_task_obs(m, s, TASK, o.obs);
-  w_make_carry<NT>(m, pl, s, o.carry);
+  w_make_carry<NT>(m, pl, s, s.carry);
   SYNC();
 }
 
@@ -1051,7 +1085,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   WT_START();
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
-  for (int k = tid; k < NCARRY; k += NT) o.carry[k] = st.carry[SC(st, k, e)];
+  for (int k = tid; k < NCARRY; k += NT) s.carry[k] = st.carry[SC(st, k, e)];
   SYNC();
   if (sub_begin > 0) {
     /* resume: the state after the previous unit's substeps, and the ctrl it applied */
@@ -1095,11 +1129,11 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
         for (int k = 0; k < 7; k++) traj[k] = o.a[k];
       }
       double out[7];
-      k_pid_task_ctrl(traj, o.carry, s.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
+      k_pid_task_ctrl(traj, s.carry, s.qvel, c.gains, m->act_ctrlrange[m->nu - 1][1], out);
       for (int k = 0; k < 6; k++) ctrl[k] = out[k];
       if (m->nu > 6) ctrl[6] = out[6];
     } else if (TASK == UR3E_TASK_MOVE_L) {
-      k_move_l_ctrl(m, o.a, o.carry, s.qpos, s.qvel, c.gains, ctrl);
+      k_move_l_ctrl(m, o.a, s.carry, s.qpos, s.qvel, c.gains, ctrl);
     } else if (TASK == UR3E_TASK_MOVE_J) {
       for (int k = 0; k < 6; k++) {
         double q = s.qpos[k];
@@ -1164,7 +1198,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       w_step_pre<NT>(m, s);
       continue;
     }
-    w_make_carry<NT>(m, pl, s, o.carry);
+    w_make_carry<NT>(m, pl, s, s.carry);
     SYNC();
     WT(25);
     if (!k_is_gym(TASK)) {
@@ -1229,11 +1263,11 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   }
 }
 
-template <int NT>
+template <int NT, class KS = KSL>
 __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                    KConfig c, KState st, const unsigned char* __restrict__ mask,
                                                    double* __restrict__ obs_out) {
-  __shared__ KSL s;
+  __shared__ KS s;
   __shared__ WOut o;
   const int e = blockIdx.x;
   if (e >= st.n) return;
@@ -1246,11 +1280,14 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
 
 /* one env per workgroup; a compact-tier (KS::BAIL) env that overflows is queued on ovf_list
    for w_env_step_list and writes nothing */
-/* waves per SIMD the compact tier is compiled for: 2 caps it at 256 registers (arch + acc) so two
-   envs share a SIMD when LDS allows (the overlaid layout) */
+/* waves per SIMD the compact tier is compiled for: 3 caps it at 168 registers (arch + acc) so that
+   three envs share a SIMD when LDS allows (the overlaid layout in dynamic LDS, w_dyn_lds) */
 #ifndef W_COMPACT_WPE
-#define W_COMPACT_WPE 2
+#define W_COMPACT_WPE 3
 #endif
+/* the mesh-capable compact tier keeps two waves per SIMD: its GJK (simplex in private memory) does not
+   fit 168 registers without spilling most of the forward pass */
+#define W_WPE_OF(KS) (KS::MESHES ? 2 : W_COMPACT_WPE)
 /* diagnostic build only (-DUR3E_WAVE_TRACE): per env of the last step launch, lane 0's
    s_memrealtime (100 MHz) at start and end, XCC_ID:HW_ID, and did_reset | ncon << 8 | blockIdx << 32 */
 #ifdef UR3E_WAVE_TRACE
@@ -1275,15 +1312,15 @@ KD int k_xcd_env(int b, int n) {
 }
 
 template <int NT, class KS, int TK = -1>
-__global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
+__global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                   KConfig c, KState st, const double* __restrict__ actions, int adim,
                                                   double* __restrict__ obs_out, double* __restrict__ rew_out,
                                                   unsigned char* __restrict__ term_out,
                                                   unsigned char* __restrict__ trunc_out,
                                                   double* __restrict__ tobs_out, int* __restrict__ ovf_list,
                                                   int* __restrict__ ovf_count) {
-  __shared__ KS s;
-  __shared__ WOut o;
+  KS& s = w_smem<KS>();
+  WOut& o = w_wout<KS>();
   if ((int)blockIdx.x >= st.n) return;
   const int e = k_xcd_env((int)blockIdx.x, st.n);
   if (st.route && __builtin_amdgcn_readfirstlane(st.route[e])) return; /* stepped by the grasp tier */
@@ -1345,7 +1382,7 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_COMPACT_WPE : 1)) void w_env_s
 KD int w_flag_poll(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 template <int NT, class KS, int TK = -1>
-__global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_model_t* __restrict__ m,
+__global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_model_t* __restrict__ m,
                                                                   const KPlan* __restrict__ pl, KConfig c, KState st,
                                                                   const double* __restrict__ actions, int adim,
                                                                   double* __restrict__ obs_out,
@@ -1356,8 +1393,8 @@ __global__ __launch_bounds__(NT, W_COMPACT_WPE) void w_env_step_q(const ur3e_mod
                                                                   int* ovf_ctl, int* qctl, int* flags,
                                                                   double* __restrict__ mid,
                                                                   unsigned long long* qstats) {
-  __shared__ KS s;
-  __shared__ WOut o;
+  KS& s = w_smem<KS>();
+  WOut& o = w_wout<KS>();
   __shared__ int s_u, s_epoch, s_flag, s_from;
   const int tid = threadIdx.x;
   const int n = st.n, fs = c.frame_skip;
@@ -1599,13 +1636,13 @@ __global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __r
   }
 }
 
-template <int NT>
+template <int NT, class KS = KSL>
 __global__ __launch_bounds__(NT) void w_env_set_state(const ur3e_model_t* __restrict__ m,
                                                        const KPlan* __restrict__ pl, KConfig c, KState st,
                                                        const double* __restrict__ qpos,
                                                        const double* __restrict__ qvel,
                                                        const double* __restrict__ warm) {
-  __shared__ KSL s;
+  __shared__ KS s;
   __shared__ WOut o;
   const int e = blockIdx.x, tid = threadIdx.x;
   if (e >= st.n) return;
@@ -1619,7 +1656,7 @@ __global__ __launch_bounds__(NT) void w_env_set_state(const ur3e_model_t* __rest
   for (int k = tid; k < m->nu; k += NT) s.ctrl[k] = 0;
   SYNC();
   w_forward<NT>(m, pl, s);
-  w_make_carry<NT>(m, pl, s, o.carry);
+  w_make_carry<NT>(m, pl, s, s.carry);
   SYNC();
   w_commit<NT>(m, c, st, e, s, o, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
 }
@@ -1676,6 +1713,8 @@ struct ur3e_batch {
   int wave_nt; /* 0: lane-per-env kernels (v1); 64/128: workgroup-per-env kernels (v2) */
   int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
+  int mesh;      /* the mesh-capable tier set (KSS_NV_M / KSG_NV_M / KSL_M): main.xml's tree with convex
+                    meshes, or a model beyond K_NG geoms / W_MAXCAND candidate pairs */
   int* d_ovf_list;
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
   unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier,
@@ -1731,9 +1770,9 @@ extern "C" const char* ur3e_last_error(void) { return g_err.c_str(); }
 
 static int check_model(const ur3e_model_t* m) {
   if (m->version != UR3E_MODEL_VERSION) return fail(UR3E_EMODEL, "model image version mismatch");
-  if (m->nq > K_NQ || m->nv > K_NV || m->nbody > K_NB || m->njnt > K_NJ || m->ngeom > K_NG ||
+  if (m->nq > K_NQ || m->nv > K_NV || m->nbody > K_NB || m->njnt > K_NJ || m->ngeom > K_NG_MESH ||
       m->nsite > K_NS || m->nu > K_NU)
-    return fail(UR3E_EMODEL, "model exceeds kernel capacities (K_NQ/K_NV/K_NB/K_NJ/K_NG/K_NS/K_NU)");
+    return fail(UR3E_EMODEL, "model exceeds kernel capacities (K_NQ/K_NV/K_NB/K_NJ/K_NG_MESH/K_NS/K_NU)");
   if (m->ncpair > UR3E_MAXCPAIR) return fail(UR3E_EMODEL, "too many collision candidates");
   return UR3E_OK;
 }
@@ -1843,13 +1882,38 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
      only the full-capacity layout keeps, so a handle with sensors on runs the full-capacity tier */
   int tiered = cfg->envs_per_block == 0 && !cfg->sensors;
   int wave_nt = cfg->envs_per_block == 0 ? 128 : (cfg->envs_per_block == -64 ? 64 : (cfg->envs_per_block < 0 ? 128 : 0));
-  if (wave_nt && model->ncpair > W_MAXCAND) return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
+  KPlan plan;
+  build_plan(model, &plan);
+  int main_tree = model->nv == UR3E_MAIN_NV && plan.max_jntnum <= 1;
+  for (int i = 0; i < model->nv && main_tree; i++)
+    if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) main_tree = 0;
+  if (model->nbody != UR3E_MAIN_NB) main_tree = 0;
+  for (int i = 0; i < model->nbody && main_tree; i++)
+    if (model->body_parentid[i] != ur3e_main_body_parent[i] || model->body_dofnum[i] != ur3e_main_body_dofnum[i] ||
+        model->body_jntadr[i] != ur3e_main_body_jntadr[i])
+      main_tree = 0;
+  /* the mesh-capable tier set: main.xml's tree with convex meshes (its compact and grasp tiers settle
+     separated mesh pairs themselves), or any model beyond the default geom / candidate capacities (which
+     then runs the full-capacity tier only, unless it has main.xml's tree) */
+  int has_mesh = 0;
+  for (int g = 0; g < model->ngeom; g++) has_mesh |= model->geom_type[g] == UR3E_GEOM_MESH;
+  const int mesh = model->ngeom > K_NG || model->ncpair > W_MAXCAND || (main_tree && has_mesh);
+  if (mesh) {
+    if (model->ncpair > W_MAXCAND_MESH) return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
+    if (wave_nt == 64 || !wave_nt)
+      return fail(UR3E_EINVAL, "this model runs in the mesh-capable layouts: envs_per_block 0 or -128");
+    if (!main_tree) tiered = 0; /* the compact tiers are specialised for main.xml's tree */
+  } else if (wave_nt && model->ncpair > W_MAXCAND) {
+    return fail(UR3E_EMODEL, "too many collision candidates for v2 kernels");
+  }
   HIPCHK(hipSetDevice(device));
   ur3e_batch* b = new ur3e_batch();
   b->device = device;
   b->n = n_envs;
   b->wave_nt = wave_nt;
   b->tiered = tiered;
+  b->mesh = mesh;
+  b->main_tree = main_tree;
   b->host_model = *model;
   b->timed = 0;
   b->timing = 0;
@@ -1869,16 +1933,6 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.sensors = cfg->sensors != 0;
   c.spin_limit = 0;
   c.leave_static = 0;
-  KPlan plan;
-  build_plan(model, &plan);
-  b->main_tree = model->nv == UR3E_MAIN_NV && plan.max_jntnum <= 1;
-  for (int i = 0; i < model->nv && b->main_tree; i++)
-    if (plan.dof_anc_mask[i] != ur3e_main_dof_anc_mask[i]) b->main_tree = 0;
-  if (model->nbody != UR3E_MAIN_NB) b->main_tree = 0;
-  for (int i = 0; i < model->nbody && b->main_tree; i++)
-    if (model->body_parentid[i] != ur3e_main_body_parent[i] || model->body_dofnum[i] != ur3e_main_body_dofnum[i] ||
-        model->body_jntadr[i] != ur3e_main_body_jntadr[i])
-      b->main_tree = 0;
   for (int k = 0; k < 12; k++) {
     c.gains.task[k] = cfg->task_gains[k];
     c.gains.joint[k] = cfg->joint_gains[k];
@@ -1931,7 +1985,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->hstep = 0; b->last_route = -1;
   if (b->grasp) {
     int per_cu = 0, cus = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)w_env_step_list<64, KSG_NV>, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, b->mesh ? (const void*)w_env_step_list<64, KSG_NV_M> : (const void*)w_env_step_list<64, KSG_NV>, 64, 0));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     b->g_grid = per_cu * cus;
     if (b->g_grid < 1) b->g_grid = 1;
@@ -1965,7 +2020,9 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->q_grid = 0;
   if (b->queued) {
     int per_cu = 0, cus = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)w_env_step_q<64, KSS_NV>, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, b->mesh ? (const void*)w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2> : (const void*)w_env_step_q<64, KSS_NV>,
+        64, b->mesh ? w_dyn_lds<KSS_NV_M>() : w_dyn_lds<KSS_NV>()));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     b->q_grid = per_cu * cus;
     if (b->q_grid < 1) b->q_grid = 1;
@@ -2039,7 +2096,10 @@ static int grid_of(const ur3e_batch* b) { return (b->n + b->cfg.epb - 1) / b->cf
 extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* d_obs, void* stream) {
   if (!b) return fail(UR3E_EINVAL, "null handle");
   HIPCHK(hipSetDevice(b->device));
-  if (b->wave_nt == 128)
+  if (b->wave_nt == 128 && b->mesh)
+    hipLaunchKernelGGL((w_env_reset<128, KSL_M>), dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model, b->d_plan,
+                       b->cfg, b->st, d_mask, d_obs);
+  else if (b->wave_nt == 128)
     hipLaunchKernelGGL(w_env_reset<128>, dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model, b->d_plan, b->cfg,
                        b->st, d_mask, d_obs);
   else if (b->wave_nt == 64)
@@ -2049,6 +2109,92 @@ extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* 
     hipLaunchKernelGGL(k_env_reset, dim3(grid_of(b)), dim3(64), 0, (hipStream_t)stream, b->d_model, b->cfg, b->st,
                        d_mask, d_obs);
   HIPCHK(hipGetLastError());
+  return UR3E_OK;
+}
+
+/* the tiered step's launches for one tier set (compact KSC, grasp KSG, full capacity KSF): the grasp
+   pre-pass (pre), the compact tier, the grasp tier over the compact tier's bails, the full-capacity tier
+   over the grasp tier's (or, without the grasp tier, the compact tier's) */
+template <class KSC, class KSG, class KSF>
+static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool pre, const double* d_actions, int adim,
+                        double* d_obs, double* d_reward, uint8_t* d_terminated, uint8_t* d_truncated,
+                        double* d_terminal_obs) {
+  const int task = b->cfg.task;
+  if (pre) {
+    /* fork: envs routed by the last step's hints run in the grasp tier on the side stream while
+       the compact tier (which skips them) runs here */
+    HIPCHK(hipEventRecord(b->ev_fork, st));
+    HIPCHK(hipStreamWaitEvent(b->side, b->ev_fork, 0));
+    hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
+                       b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                       b->d_pred_list, b->d_pred_ctl, b->d_ovf_total + 2, b->d_ovf2_list, b->d_ovf2_ctl,
+                       nullptr, nullptr);
+    HIPCHK(hipEventRecord(b->ev_join, b->side));
+  }
+  /* main.xml: dof count and tree specialised at compile time; the gym ur3e-v2 and scripted
+     move_l_mug tasks also get kernels specialised for their task (the other tasks' controller and
+     epilogue code folds away, which keeps the register budget for the task that runs) */
+  if constexpr (KSC::MESHES) { /* the mesh-capable set: generic kernels, plus the queue's ur3e-v2 one */
+    if (b->queued && task == UR3E_TASK_GYM_V2)
+      hipLaunchKernelGGL((w_env_step_q<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st,
+                         b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
+                         d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
+                         b->d_mid, b->d_ovf_total + 3);
+    else if (b->queued)
+      hipLaunchKernelGGL((w_env_step_q<64, KSC>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan,
+                         b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
+                         b->d_ovf_total + 3);
+    else
+      hipLaunchKernelGGL((w_env_step<64, KSC>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan, b->cfg,
+                         kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf_list, b->d_ovf_ctl);
+  } else if (b->queued) { /* substep work queue (w_env_step_q) */
+    if (task == UR3E_TASK_GYM_V2)
+      hipLaunchKernelGGL((w_env_step_q<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st,
+                         b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
+                         d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
+                         b->d_mid, b->d_ovf_total + 3);
+    else
+      hipLaunchKernelGGL((w_env_step_q<64, KSC>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan,
+                         b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
+                         b->d_ovf_total + 3);
+  } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
+    hipLaunchKernelGGL((w_env_step<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model,
+                       b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                       d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+  } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
+    hipLaunchKernelGGL((w_env_step<64, KSC, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model,
+                       b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                       d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+  } else if (b->main_tree)
+    hipLaunchKernelGGL((w_env_step<64, KSC>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan, b->cfg,
+                       kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                       b->d_ovf_list, b->d_ovf_ctl);
+  else
+    hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), w_dyn_lds<KSS>(), st, b->d_model, b->d_plan, b->cfg, kst,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_ctl);
+  int grid = b->n < 512 ? b->n : 512;
+  if (b->grasp) {
+    if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
+    /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier, whose
+       workgroup 0 also snapshots the routing hints for the next step */
+    const int post_grid = pre || b->g_grid < W_GRASP_IDLE_GRID ? b->g_grid : W_GRASP_IDLE_GRID;
+    hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(post_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+                       b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
+                       nullptr);
+    hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
+                       b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                       b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
+                       b->d_pred_ctl);
+  } else {
+    hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
+                       b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr);
+  }
   return UR3E_OK;
 }
 
@@ -2092,67 +2238,16 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
       pre = capturing || (b->last_route >= 0 && b->hstep - b->last_route < W_ROUTE_HOLD);
       if (!pre) kst.route = nullptr;
     }
-    if (pre) {
-      /* fork: envs routed by the last step's hints run in the grasp tier on the side stream while
-         the compact tier (which skips them) runs here */
-      HIPCHK(hipEventRecord(b->ev_fork, st));
-      HIPCHK(hipStreamWaitEvent(b->side, b->ev_fork, 0));
-      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(b->g_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
-                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_pred_list, b->d_pred_ctl, b->d_ovf_total + 2, b->d_ovf2_list, b->d_ovf2_ctl,
-                         nullptr, nullptr);
-      HIPCHK(hipEventRecord(b->ev_join, b->side));
-    }
-    /* main.xml: dof count and tree specialised at compile time; the gym ur3e-v2 and scripted
-       move_l_mug tasks also get kernels specialised for their task (the other tasks' controller and
-       epilogue code folds away, which keeps the register budget for the task that runs) */
-    if (b->queued) { /* substep work queue (w_env_step_q) */
-      if (task == UR3E_TASK_GYM_V2)
-        hipLaunchKernelGGL((w_env_step_q<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), 0, st,
-                           b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
-                           d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
-                           b->d_mid, b->d_ovf_total + 3);
-      else
-        hipLaunchKernelGGL((w_env_step_q<64, KSS_NV>), dim3(b->q_grid), dim3(64), 0, st, b->d_model, b->d_plan,
-                           b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                           d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
-                           b->d_ovf_total + 3);
-    } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
-      hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), 0, st, b->d_model,
-                         b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
-    } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
-      hipLaunchKernelGGL((w_env_step<64, KSS_NV, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), 0, st, b->d_model,
-                         b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
-    } else if (b->main_tree)
-      hipLaunchKernelGGL((w_env_step<64, KSS_NV>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg,
-                         kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, b->d_ovf_ctl);
-    else
-      hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), 0, st, b->d_model, b->d_plan, b->cfg, kst,
-                         d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                         b->d_ovf_ctl);
-    int grid = b->n < 512 ? b->n : 512;
-    if (b->grasp) {
-      if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
-      /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier, whose
-         workgroup 0 also snapshots the routing hints for the next step */
-      const int post_grid = pre || b->g_grid < W_GRASP_IDLE_GRID ? b->g_grid : W_GRASP_IDLE_GRID;
-      hipLaunchKernelGGL((w_env_step_list<64, KSG_NV>), dim3(post_grid), dim3(64), 0, st, b->d_model, b->d_plan,
-                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
-                         nullptr);
-      hipLaunchKernelGGL((w_env_step_list<128, KSL>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
-                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
-                         b->d_pred_ctl);
-    } else {
-      hipLaunchKernelGGL((w_env_step_list<128, KSL>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
-                         b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr);
-    }
-  } else if (b->wave_nt == 128)
+    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+                                                                      d_terminated, d_truncated, d_terminal_obs)
+                           : launch_tiers<KSS_NV, KSG_NV, KSL>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+                                                                d_terminated, d_truncated, d_terminal_obs);
+    if (rc != UR3E_OK) return rc;
+  } else if (b->wave_nt == 128 && b->mesh)
+    hipLaunchKernelGGL((w_env_step<128, KSL_M>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
+                       b->d_ovf_ctl);
+  else if (b->wave_nt == 128)
     hipLaunchKernelGGL((w_env_step<128, KSL>), dim3(b->n), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg, b->st,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
                        b->d_ovf_ctl);
@@ -2194,7 +2289,10 @@ extern "C" int ur3e_batch_set_state(ur3e_batch_t* b, const double* d_qpos, const
                                     const double* d_warm, void* stream) {
   if (!b || !d_qpos || !d_qvel) return fail(UR3E_EINVAL, "null handle or state");
   HIPCHK(hipSetDevice(b->device));
-  if (b->wave_nt == 128)
+  if (b->wave_nt == 128 && b->mesh)
+    hipLaunchKernelGGL((w_env_set_state<128, KSL_M>), dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model,
+                       b->d_plan, b->cfg, b->st, d_qpos, d_qvel, d_warm);
+  else if (b->wave_nt == 128)
     hipLaunchKernelGGL(w_env_set_state<128>, dim3(b->n), dim3(128), 0, (hipStream_t)stream, b->d_model, b->d_plan,
                        b->cfg, b->st, d_qpos, d_qvel, d_warm);
   else if (b->wave_nt == 64)
@@ -2329,13 +2427,20 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
   HIPCHK(hipSetDevice(b->device));
   const void* fn;
   int nt;
+  size_t dyn = 0; /* the compact tier's working set is dynamic LDS (w_dyn_lds) */
   if (b->tiered) {
     nt = 64;
-    fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
-                   : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
+    if (b->mesh) {
+      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2> : (const void*)w_env_step<64, KSS_NV_M>;
+      dyn = w_dyn_lds<KSS_NV_M>();
+    } else {
+      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
+                     : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
+      dyn = b->main_tree ? w_dyn_lds<KSS_NV>() : w_dyn_lds<KSS>();
+    }
   } else if (b->wave_nt == 128) {
     nt = 128;
-    fn = (const void*)w_env_step<128, KSL>;
+    fn = b->mesh ? (const void*)w_env_step<128, KSL_M> : (const void*)w_env_step<128, KSL>;
   } else if (b->wave_nt == 64) {
     nt = 64;
     fn = (const void*)w_env_step<64, KSL>;
@@ -2346,10 +2451,10 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
   hipFuncAttributes attr;
   HIPCHK(hipFuncGetAttributes(&attr, fn));
   int blocks = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, nt, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, nt, dyn));
   const int envs = (b->tiered || b->wave_nt) ? blocks : blocks * nt; /* v1: one env per lane */
   if (envs_per_cu) *envs_per_cu = envs;
-  if (lds_bytes) *lds_bytes = (int)attr.sharedSizeBytes;
+  if (lds_bytes) *lds_bytes = (int)(attr.sharedSizeBytes + dyn);
   if (regs) *regs = attr.numRegs;
   return UR3E_OK;
 }

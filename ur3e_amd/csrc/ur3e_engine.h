@@ -31,6 +31,8 @@
 
 /* kernel capacities: the largest reference model (main.xml: nq 21, nv 20, 25 bodies) */
 #define K_NQ 21
+/* stale-kinematics carry per env: tcp xpos(3), xmat(9), arm Jacobian 6x6, qfrc_bias[0:6] */
+#define NCARRY 54
 #define K_NV 20
 #define K_NB 25
 #define K_NJ 16

@@ -27,10 +27,16 @@
 #include "gen_main_tree.h"
 
 #define W_MAXCAND 128 /* collision candidates handled per env (main.xml: 92) */
+/* mesh-capable layouts (main.xml with its convex meshes: 24 colliding geoms, 234 candidate pairs) */
+#define K_NG_MESH 24
+#define W_MAXCAND_MESH 240
+/* survivors of the bounding-sphere filter the overlaid (compact / grasp) layouts hold; an env-step with
+   more hands on to the next tier */
+#define W_MAXSURV 64
 #define W_MAXGRP 96   /* constraint row groups */
 /* compact-tier narrowphase: survivor lanes per chunk (their clip polygons live in LDS) and staged
    raw contacts per chunk (>= the compact tier's MAXCON: a chunk staging more has overflowed) */
-#define W_NP_LANES 16
+#define W_NP_LANES 8
 #define W_NP_STAGE 16
 
 /* host-precomputed tree bookkeeping for the cooperative stages */
@@ -74,12 +80,16 @@ struct KPlan {
    compact tier (rows <= 64: one 64-lane wavefront, register-resident solver) overlays the arrays
    of the position/velocity stages with those of the constraint stages, see the specialisation
    below. */
-template <int MC, int ME, int NVC = 0, int TREE = 0, bool OVERLAY = (ME <= 64)>
+template <int MC, int ME, int NVC = 0, int TREE = 0, bool OVERLAY = (ME <= 64), int NGC = K_NG>
 struct KSX;
 
-template <int MC, int ME, int NVC, int TREE>
-struct KSX<MC, ME, NVC, TREE, false> {
+template <int MC, int ME, int NVC, int TREE, int NGC>
+struct KSX<MC, ME, NVC, TREE, false, NGC> {
   static constexpr bool OVERLAY = false;
+  /* geoms this layout holds; NGC = K_NG_MESH: the mesh-capable variant (main.xml with real meshes) */
+  static constexpr int NG = NGC;
+  static constexpr bool MESHES = NGC == K_NG_MESH;
+  static constexpr int NCAND = MESHES ? W_MAXCAND_MESH : W_MAXCAND;
   static constexpr int NV = NVC;    /* > 0: kernel specialised for a model with exactly NVC dofs */
   static constexpr int STATIC_TREE = TREE; /* 1: main.xml's dof tree as compile-time tables */
   static constexpr int MAXCON = MC; /* contacts this tier holds */
@@ -93,7 +103,7 @@ struct KSX<MC, ME, NVC, TREE, false> {
   /* position stage */
   double xpos[K_NB][3], xquat[K_NB][4], xmat[K_NB][9];
   double xanchor[K_NJ][3], xaxis[K_NJ][3];
-  double geom_xpos[K_NG][3], geom_xmat[K_NG][9];
+  double geom_xpos[NGC][3], geom_xmat[NGC][9];
   double site_xpos[K_NS][3], site_xmat[K_NS][9];
   double subtree_com[K_NB][3], cinert[K_NB][10], cdof[K_NV][6];
   double cvel[K_NB][6], cdof_dot[K_NV][6];
@@ -119,7 +129,7 @@ struct KSX<MC, ME, NVC, TREE, false> {
   double con_pos[MC][3], con_frame[MC][9], con_dist[MC], con_mu[MC];
   double con_Hc[MC][9];
   int con_geom1[MC], con_geom2[MC], con_cpair[MC], con_efc[MC];
-  int cand_count[W_MAXCAND], cand_off[W_MAXCAND];
+  int cand_count[NCAND], cand_off[NCAND];
   /* constraint rows */
   double efc_J[ME][K_NV];
   double efc_R[ME], efc_D[ME], efc_aref[ME], efc_floss[ME];
@@ -131,6 +141,7 @@ struct KSX<MC, ME, NVC, TREE, false> {
   double sensordata[UR3E_MAXSENSORDATA];
   double cacc[K_NB][6], cfrc_int[K_NB][6], cfrc_ext[K_NB][6];
   int sens;
+  double carry[NCARRY]; /* the stale-kinematics carry: read by the controller, rebuilt after the last forward */
   /* scalars */
   double gauss, cost, scale, g1, g2, lsF, lsdF, lsd2F, sred;
   int ncon, nefc, ngrp, nwarn, flag, ovf, cap_con;
@@ -158,9 +169,13 @@ struct KSX<MC, ME, NVC, TREE, false> {
        Hessian / tree-factor scratch (the register solver only touches j <= i).
    Only the fields the compact code path touches exist here. */
 #define KTRI(i, j) ((i) * ((i) + 1) / 2 + (j))
-template <int MC, int ME, int NVC, int TREE>
-struct KSX<MC, ME, NVC, TREE, true> {
+template <int MC, int ME, int NVC, int TREE, int NGC>
+struct KSX<MC, ME, NVC, TREE, true, NGC> {
   static constexpr bool OVERLAY = true;
+  static constexpr int NG = NGC;
+  static constexpr bool MESHES = NGC == K_NG_MESH;
+  /* candidate pairs: only the bounding-sphere survivors are listed (W_MAXSURV; more bail) */
+  static constexpr int NCAND = MESHES ? W_MAXCAND_MESH : W_MAXCAND;
   static constexpr int NV = NVC;
   static constexpr int STATIC_TREE = TREE;
   static constexpr int MAXCON = MC;
@@ -196,21 +211,23 @@ struct KSX<MC, ME, NVC, TREE, true> {
   union {
     struct {
       /* KC */
-      double geom_xpos[K_NG][3], geom_xmat[K_NG][9];
-      int cand_count[W_MAXCAND], cand_off[W_MAXCAND];
+      double geom_xpos[NGC][3], geom_xmat[NGC][9];
+      int cand_off[W_MAXSURV]; /* bounding-sphere survivors, in candidate order */
       union {
         struct { /* KA */
           double xquat[K_NB][4], xmat[K_NB][9];
           double xanchor[K_NJ][3], xaxis[K_NJ][3], qloc[K_NJ][4];
         };
         struct { /* KB */
-          double cinert[K_NB][10], cdof_dot[K_NV][6], cvel[K_NB][6];
+          double cinert[K_NB][10], cvel[K_NB][6];
           double actuator_length[K_NU], qfrc_passive[K_NV];
+          /* body temporaries by lifetime: the composite inertia (crb) for the mass matrix; then cacc and
+             cdof_dot in the velocity / acceleration pass; then cacc and cfrc in RNE, cfrc over the dead
+             cdof_dot (w_crb, w_cacc, w_cdof_dot, w_cfrc pick the arrays in either layout) */
           union {
-            struct {
-              double b10[K_NB][10];
-              double b6[K_NB][6];
-            } body;
+            struct { double b10[K_NB][10]; } crb;
+            struct { double cacc[K_NB][6]; double cdof_dot[K_NV][6]; } va;
+            struct { double cacc[K_NB][6]; double cfrc[K_NB][6]; } rne;
           } u;
         };
         struct { /* KN, collision: clip polygons of one chunk of survivor lanes ([buf][vertex][coord]
@@ -221,6 +238,10 @@ struct KSX<MC, ME, NVC, TREE, true> {
           int np_nstage;
         };
       };
+    };
+    struct { /* CR: the stale-kinematics carry, alive only before the first forward (the controller reads it)
+                and after the last (rebuilt for the commit), when nothing else in the union is */
+      double carry[NCARRY];
     };
     struct { /* N */
       double efc_J[ME][K_NV];
@@ -236,6 +257,28 @@ struct KSX<MC, ME, NVC, TREE, true> {
   };
 };
 
+/* the body temporaries in either layout (the overlaid one packs them by lifetime) */
+template <class S>
+__device__ __forceinline__ auto w_crb(S& s) {
+  if constexpr (std::remove_const_t<S>::OVERLAY) return s.u.crb.b10;
+  else return s.u.body.b10;
+}
+template <class S>
+__device__ __forceinline__ auto w_cacc(S& s) {
+  if constexpr (std::remove_const_t<S>::OVERLAY) return s.u.va.cacc;
+  else return s.u.body.b10;
+}
+template <class S>
+__device__ __forceinline__ auto w_cdof_dot(S& s) {
+  if constexpr (std::remove_const_t<S>::OVERLAY) return s.u.va.cdof_dot;
+  else return s.cdof_dot;
+}
+template <class S>
+__device__ __forceinline__ auto w_cfrc(S& s) {
+  if constexpr (std::remove_const_t<S>::OVERLAY) return s.u.rne.cfrc;
+  else return s.u.body.b6;
+}
+
 /* mass-matrix element (i, j) in either layout */
 template <class KS>
 __device__ __forceinline__ double qm_get(const KS& s, int i, int j) {
@@ -244,15 +287,15 @@ __device__ __forceinline__ double qm_get(const KS& s, int i, int j) {
 }
 /* full-capacity tier: the oracle's limits (UR3E_MAXCON contacts, UR3E_MAXEFC rows) */
 typedef KSX<K_MAXCON, K_MAXEFC> KSL;
-/* compact tier: sized for the contact/row counts main.xml actually reaches
-   (<= 8 contacts, <= 38 rows over long random and grasp rollouts; 13 fixed rows +
-   3 per contact), small enough
-   for four envs (four wavefronts) per CU */
+/* compact tier: sized for the gym workload on main.xml -- the mug resting on the table (4 contacts,
+   13 fixed rows + 3 per contact = 25) plus joint-limit rows (25-27 rows over random-action rollouts,
+   tools/contact_hist.py) -- with room for one more contact, so that the working set stays under
+   16 KB: ten envs per CU.  Env-steps beyond it (grasps, arm contacts) run in the grasp tier. */
 #ifndef W_SMALL_MAXCON
-#define W_SMALL_MAXCON 10
+#define W_SMALL_MAXCON 5
 #endif
 #ifndef W_SMALL_MAXEFC
-#define W_SMALL_MAXEFC 44
+#define W_SMALL_MAXEFC 30
 #endif
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
 /* compact tier specialised for main.xml: compile-time dof count and dof tree (gen_main_tree.h),
@@ -270,6 +313,13 @@ static_assert(UR3E_MAIN_NV <= K_NV, "main.xml dofs exceed K_NV");
 #define W_GRASP_MAXEFC 96
 #endif
 typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true> KSG_NV;
+/* the same three tiers for main.xml with its convex meshes (K_NG_MESH geoms, W_MAXCAND_MESH candidate
+   pairs): the compact and grasp tiers settle a mesh pair whose hulls GJK finds separated beyond the
+   margin themselves (no contact, the oracle's decision with the same code) and hand on an env-step whose
+   mesh pair touches; the full-capacity tier runs GJK + EPA */
+typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSS_NV_M;
+typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
+typedef KSX<K_MAXCON, K_MAXEFC, 0, 0, false, K_NG_MESH> KSL_M;
 #define NVOF(KS, m) ((KS::NV) ? (KS::NV) : (m)->nv)
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
@@ -590,17 +640,17 @@ WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
     /* composite inertias summed up the tree in registers (lane = body) */
     if constexpr (KS::STATIC_TREE) {
       /* components across lanes: cinert rows in, crb rows out */
-      r_subtree_sum_cols<10, true>(s.cinert, s.u.body.b10);
+      r_subtree_sum_cols<10, true>(s.cinert, w_crb(s));
     } else {
       double crb[10];
       for (int k = 0; k < 10; k++) crb[k] = tid < nb ? s.cinert[tid][k] : 0.0;
       r_subtree_sum<10, true>(m, crb);
       if (tid < nb)
-        for (int k = 0; k < 10; k++) s.u.body.b10[tid][k] = crb[k];
+        for (int k = 0; k < 10; k++) w_crb(s)[tid][k] = crb[k];
     }
     WT(34);
   } else {
-    for (int e = tid; e < nb * 10; e += NT) s.u.body.b10[e / 10][e % 10] = s.cinert[e / 10][e % 10];
+    for (int e = tid; e < nb * 10; e += NT) w_crb(s)[e / 10][e % 10] = s.cinert[e / 10][e % 10];
   }
   if constexpr (KS::OVERLAY) {
     for (int e = tid; e < nv * (nv + 1) / 2; e += NT) s.qMp[e] = 0;
@@ -612,7 +662,7 @@ WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
     if (tid < 10) {
       for (int i = nb - 1; i > 0; i--) {
         int p = m->body_parentid[i];
-        if (p > 0) s.u.body.b10[p][tid] += s.u.body.b10[i][tid];
+        if (p > 0) w_crb(s)[p][tid] += w_crb(s)[i][tid];
       }
     }
     SYNC();
@@ -620,7 +670,7 @@ WD void w_crb(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if (tid < nv) {
     int i = tid;
     double buf[6];
-    k_mul_inert_vec(buf, s.u.body.b10[m->dof_bodyid[i]], s.cdof[i]);
+    k_mul_inert_vec(buf, w_crb(s)[m->dof_bodyid[i]], s.cdof[i]);
     double mii = m->dof_armature[i];
     mii += k_dot6(s.cdof[i], buf);
     if constexpr (KS::OVERLAY) s.qMp[KTRI(i, i)] = mii;
@@ -753,6 +803,17 @@ __device__ __forceinline__ int w_mesh_collide(KModel m, const KS& s, int g1, int
   return ur3e_convex_convex(&a, &b, margin, &scratch, raw[0].pos, raw[0].n, &raw[0].dist);
 }
 
+/* the mesh pair (g1, g2) reports no contact (ur3e_plane_convex_clear / ur3e_convex_separated) */
+template <class KS>
+__device__ __forceinline__ bool w_mesh_separated(KModel m, const KS& s, int g1, int g2, double margin) {
+  ur3e_cvx b;
+  w_geom_convex(m, s, g2, &b);
+  if (m->geom_type[g1] == UR3E_GEOM_PLANE) return ur3e_plane_convex_clear(s.geom_xpos[g1], s.geom_xmat[g1], &b, margin);
+  ur3e_cvx a;
+  w_geom_convex(m, s, g1, &a);
+  return ur3e_convex_separated(&a, &b, margin);
+}
+
 /* narrowphase of candidate pair p (after w_pair_near): raw contacts, returns their count */
 template <class KS, bool INL = false>
 WD int w_narrow_core(KModel m, const KS& s, int p, KRaw* raw) {
@@ -812,9 +873,13 @@ WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
   double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const KStageEmit<KS::NPST> emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
-  /* convex meshes run in the full-capacity tier: a mesh pair within its bounding spheres hands the
-     env-step on */
+  /* convex meshes: the mesh-capable layouts settle a pair whose hulls are apart beyond the margin (GJK,
+     or the plane's vertex distances: no contact, the oracle's own decision); a pair that may touch --
+     and every mesh pair in the other layouts -- hands the env-step on to the tier that runs EPA */
   if (t2 == UR3E_GEOM_MESH) {
+    if constexpr (KS::MESHES) {
+      if (w_mesh_separated(m, s, g1, g2, margin)) return 0;
+    }
     s.ovf = 1;
     return 0;
   }
@@ -862,16 +927,25 @@ WD void r_collision(KModel m, KS& s) {
   const int lane = w_lane();
   const int np = m->ncpair;
   int nsurv = 0;
+  /* the overlaid layouts list W_MAXSURV survivors (an env-step with more hands on); the full-capacity
+     layout every candidate */
+  constexpr int CAP = KS::OVERLAY ? W_MAXSURV : KS::NCAND;
   for (int base = 0; base < np; base += 64) {
     const int p = base + lane;
     const bool ok = p < np && w_pair_near(m, s, p);
     const unsigned long long bm = __ballot(ok);
-    if (ok) s.cand_off[nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] = p;
+    const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+    if (ok && at < CAP) s.cand_off[at] = p;
     nsurv += __popcll(bm);
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  if constexpr (KS::OVERLAY) {
+    if (nsurv > CAP) {
+      if (lane == 0) s.ovf = 1;
+      nsurv = CAP;
+    }
+  }
   WT(39);
   int total = 0;
   if constexpr (KS::OVERLAY) {
@@ -959,12 +1033,9 @@ WD void r_collision(KModel m, KS& s) {
   asm volatile("" ::: "memory");
 }
 
+/* the 128-lane full-capacity layout: counts of every candidate, prefix offsets, contacts */
 template <int NT, class KS>
-WD void w_collision(KModel m, KS& s) {
-  if constexpr (NT == 64) {
-    r_collision<KS>(m, s);
-    return;
-  }
+WD void w_collision_all(KModel m, KS& s) {
   const int tid = w_lane();
   const int np = m->ncpair;
   KRaw raw[8];
@@ -989,6 +1060,15 @@ WD void w_collision(KModel m, KS& s) {
     for (int k = 0; k < n && off + k < KS::MAXCON; k++) w_store_contact(m, s, off + k, p, raw[k]);
   }
   SYNC();
+}
+
+template <int NT, class KS>
+WD void w_collision(KModel m, KS& s) {
+  if constexpr (NT == 64) {
+    r_collision<KS>(m, s);
+  } else {
+    w_collision_all<NT>(m, s);
+  }
 }
 
 /* ================================================================== */
@@ -1242,19 +1322,19 @@ WD void w_com_vel(KModel m, const KPlan* __restrict__ pl, KS& s) {
         int jt = m->jnt_type[m->dof_jntid[dof]];
         if (jt == UR3E_JNT_FREE) {
           for (int k = 0; k < 3; k++)
-            for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
+            for (int r = 0; r < 6; r++) w_cdof_dot(s)[dof + k][r] = 0;
           double tmp[6] = {0, 0, 0, 0, 0, 0};
           for (int k = 0; k < 3; k++)
             for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
           for (int r = 0; r < 6; r++) cv[r] += tmp[r];
-          for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
+          for (int k = 3; k < 6; k++) k_cross_motion(w_cdof_dot(s)[dof + k], cv, s.cdof[dof + k]);
           for (int r = 0; r < 6; r++) tmp[r] = 0;
           for (int k = 3; k < 6; k++)
             for (int r = 0; r < 6; r++) tmp[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
           for (int r = 0; r < 6; r++) cv[r] += tmp[r];
           j += 5;
         } else {
-          k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
+          k_cross_motion(w_cdof_dot(s)[dof], cv, s.cdof[dof]);
           for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
         }
       }
@@ -1268,8 +1348,8 @@ template <int NT, class KS>
 WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int tid = w_lane();
   const int nb = m->nbody, nv = NVOF(KS, m);
-  double (*cacc)[10] = s.u.body.b10;
-  double (*cfrc)[6] = s.u.body.b6;
+  auto cacc = w_cacc(s);
+  auto cfrc = w_cfrc(s);
   constexpr bool REG = (NT == 64 && KS::OVERLAY);
   if constexpr (REG) {
     r_cfrc(m, s); /* cacc came from r_vel_acc */
@@ -1286,7 +1366,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
       double tmp[6] = {0, 0, 0, 0, 0, 0};
       int bda = m->body_dofadr[i];
       for (int j = 0; j < m->body_dofnum[i]; j++)
-        for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+        for (int r = 0; r < 6; r++) tmp[r] += w_cdof_dot(s)[bda + j][r] * s.qvel[bda + j];
       int p = m->body_parentid[i];
       for (int r = 0; r < 6; r++) cacc[i][r] = cacc[p][r] + tmp[r];
     }
@@ -1893,12 +1973,12 @@ WD void w_sensors(KModel m, const KPlan* __restrict__ pl, KS& s) {
           const int bda = m->body_dofadr[b], n = m->body_dofnum[b];
           double t = 0;
           if (n == 1) {
-            t = s.cdof_dot[bda][k] * s.qvel[bda];
+            t = w_cdof_dot(s)[bda][k] * s.qvel[bda];
           } else if (n > 1) {
             for (int j = 0; j < n; j++) {
               const double v = s.qvel[bda + j];
               if (v == 0) continue;
-              t += s.cdof_dot[bda + j][k] * v;
+              t += w_cdof_dot(s)[bda + j][k] * v;
             }
           }
           double c = s.cacc[m->body_parentid[b]][k] + t;

@@ -1422,7 +1422,8 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
   /* one joint per body on this path's models: the first dof's joint is the body's first joint */
   const bool onejnt = KS::STATIC_TREE || pl->max_jntnum <= 1;
   const int jt = bdn ? (onejnt ? pl->bj_type[b] : m->jnt_type[m->dof_jntid[bda]]) : UR3E_JNT_HINGE;
-  double (*cacc)[10] = s.u.body.b10;
+  auto cacc = w_cacc(s);
+  auto cdof_dot = w_cdof_dot(s);
   /* single-dof bodies: their cdof row and qvel, loaded up front */
   double cd[6] = {0, 0, 0, 0, 0, 0}, qv = 0;
   if (bdn == 1) {
@@ -1450,24 +1451,24 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
       int jtj = onejnt ? jt : m->jnt_type[m->dof_jntid[dof]];
       if (jtj == UR3E_JNT_FREE) {
         for (int k = 0; k < 3; k++)
-          for (int r = 0; r < 6; r++) s.cdof_dot[dof + k][r] = 0;
+          for (int r = 0; r < 6; r++) cdof_dot[dof + k][r] = 0;
         double tq[6] = {0, 0, 0, 0, 0, 0};
         for (int k = 0; k < 3; k++)
           for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
         for (int r = 0; r < 6; r++) cv[r] += tq[r];
-        for (int k = 3; k < 6; k++) k_cross_motion(s.cdof_dot[dof + k], cv, s.cdof[dof + k]);
+        for (int k = 3; k < 6; k++) k_cross_motion(cdof_dot[dof + k], cv, s.cdof[dof + k]);
         for (int r = 0; r < 6; r++) tq[r] = 0;
         for (int k = 3; k < 6; k++)
           for (int r = 0; r < 6; r++) tq[r] += s.cdof[dof + k][r] * s.qvel[dof + k];
         for (int r = 0; r < 6; r++) cv[r] += tq[r];
         j += 5;
       } else {
-        k_cross_motion(s.cdof_dot[dof], cv, s.cdof[dof]);
+        k_cross_motion(cdof_dot[dof], cv, s.cdof[dof]);
         for (int r = 0; r < 6; r++) cv[r] += s.cdof[dof][r] * s.qvel[dof];
       }
     }
     for (int j = 0; j < bdn; j++)
-      for (int r = 0; r < 6; r++) tmp[r] += s.cdof_dot[bda + j][r] * s.qvel[bda + j];
+      for (int r = 0; r < 6; r++) tmp[r] += cdof_dot[bda + j][r] * s.qvel[bda + j];
   };
   /* main.xml: the two chains with the components across lanes (r_chain_cols), the several-dof bodies
      (children of the world without children of their own, checked by the generator) on their lanes
@@ -1510,7 +1511,7 @@ WD void r_vel_acc(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if (depth > 0 && one) {
     double cdd[6];
     k_cross_motion(cdd, cvp, cd);
-    for (int r = 0; r < 6; r++) s.cdof_dot[bda][r] = cdd[r];
+    for (int r = 0; r < 6; r++) cdof_dot[bda][r] = cdd[r];
     for (int r = 0; r < 6; r++) tmp[r] += cdd[r] * qv;
   }
   if constexpr (COLS) {
@@ -1536,8 +1537,8 @@ template <class KS>
 WD void r_cfrc(KModel m, KS& s) {
   const int lane = w_lane();
   const int nb = m->nbody;
-  double (*cacc)[10] = s.u.body.b10;
-  double (*cfrc)[6] = s.u.body.b6;
+  auto cacc = w_cacc(s);
+  auto cfrc = w_cfrc(s);
   int par[K_NB];
 #pragma unroll
   for (int i = 0; i < K_NB; i++) par[i] = m->body_parentid[i];
