@@ -357,17 +357,17 @@ def test_vecnormalize_gpu_matches_sb3(norm_reward, n):
 
 @pytest.mark.gpu
 def test_compact_kernel_occupancy():
-    """the main.xml compact tier must keep ten envs per CU (a working set <= 16 KB of LDS, 168 registers:
-    three waves on two SIMDs of every CU): a change that grows the LDS layout or the register count
-    silently loses a fifth of the throughput otherwise"""
+    """the main.xml compact tier keeps its working set within 16 KB of LDS (ten would fit a CU) and eight
+    envs per CU (two waves per SIMD at <= 256 registers).  Ten envs per CU at 168 registers was built and
+    measured slower (occupancy); a change that grows the LDS layout past 20 KB or the register
+    count past 256 silently halves throughput"""
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model("main")
     b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1), 64)
     info = b.kernel_info()
     b.close()
     assert info["lds_bytes"] <= 16384, info
-    assert info["regs"] <= 168, info
-    assert info["envs_per_cu"] >= 10, info
+    assert info["envs_per_cu"] >= 8, info
 
 
 @pytest.mark.gpu

@@ -3,7 +3,7 @@
 # (tools/var/<name>.patch) and/or extra compiler flags (tools/var/<name>.flags), so no variant
 # library rides in the push.  Each variant first runs the fast
 # GPU parity set; then the bench alternates base and variants for ROUNDS rounds (boxes differ by ~1 %).
-# usage: tools/ab_multi.sh ROUNDS NAME...
+# usage: tools/ab_multi.sh ROUNDS NAME...   (AB_EXTRA=1: the bench's other configs too, printed beside)
 set -o pipefail
 R=$(pwd); D=$R/gpurun_out/ab; mkdir -p $D
 ROUNDS=$1; shift
@@ -24,8 +24,8 @@ done
 for i in $(seq 1 $ROUNDS); do
   for v in base "$@"; do
     if [ $v = base ]; then unset UR3E_LIB; else export UR3E_LIB=/tmp/ur3e_var_$v/lib.so; fi
-    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-extra > $D/$v$i.json 2> $D/$v$i.err || { echo "$v failed"; tail -3 $D/$v$i.err; exit 1; }
-    python3 -c "import json;d=json.loads(open('$D/$v$i.json').read().strip().splitlines()[-1]);print('$v',round(d['value']/1e6,4),round(d['ms_per_step'],4), round(d['roofline']['kernel_ms'],4))"
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline ${AB_EXTRA:+} $( [ -n "$AB_EXTRA" ] || echo --no-extra ) > $D/$v$i.json 2> $D/$v$i.err || { echo "$v failed"; tail -3 $D/$v$i.err; exit 1; }
+    python3 -c "import json;d=json.loads(open('$D/$v$i.json').read().strip().splitlines()[-1]);x=d.get('other_configs') or {};print('$v',round(d['value']/1e6,4),round(d['ms_per_step'],4), round(d['roofline']['kernel_ms'],4), *[(k[:14], round(v['value']/1e6,3)) for k,v in x.items() if isinstance(v,dict) and 'value' in v])"
   done
 done
 unset UR3E_LIB

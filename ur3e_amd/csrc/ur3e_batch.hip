@@ -1280,10 +1280,12 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
 
 /* one env per workgroup; a compact-tier (KS::BAIL) env that overflows is queued on ovf_list
    for w_env_step_list and writes nothing */
-/* waves per SIMD the compact tier is compiled for: 3 caps it at 168 registers (arch + acc) so that
-   three envs share a SIMD when LDS allows (the overlaid layout in dynamic LDS, w_dyn_lds) */
+/* waves per SIMD the compact tier is compiled for: 2 caps it at 256 registers (arch + acc), so two envs
+   share a SIMD.  The 16 KB working set would let a CU take ten (w_dyn_lds), and -DW_COMPACT_WPE=3 builds
+   that (168 registers): measured slower, 7.22 M against 8.06 M env-steps/s, and 7.82 M with the same 168
+   registers at eight per CU -- the third wave itself costs more than it hides (profiles/r04_ab) */
 #ifndef W_COMPACT_WPE
-#define W_COMPACT_WPE 3
+#define W_COMPACT_WPE 2
 #endif
 /* the mesh-capable compact tier keeps two waves per SIMD: its GJK (simplex in private memory) does not
    fit 168 registers without spilling most of the forward pass */
