@@ -84,6 +84,11 @@ def _host_info() -> dict:
     and lscpu's model / socket / core / thread counts."""
     info = {"machine_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:  # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max: "quota period" or "max period")
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        info["cgroup_cpu_quota"] = "unavailable"
     try:
         import subprocess
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -203,9 +208,12 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         rng = np.random.default_rng(seed + 2)
         dta = _time_oracle(oba, lambda _: rng.uniform(lo, hi, size=(n_envs_sample, 4)), all_cores_steps)
         del oba
+        quota = host.get("cgroup_cpu_quota")
+        capped = (f"; the cgroup's CPU quota is {quota} CPUs, so the {n_all} threads time-share that many"
+                  if isinstance(quota, float) and quota < n_all else "")
         all_cores = {"value": n_envs_sample * all_cores_steps / dta, "unit": "env-steps/s", "cores": n_all,
                      "sample": f"{n_envs_sample} envs x {all_cores_steps} env-steps from reset, OpenMP {n_all} "
-                               f"threads (every CPU of the affinity mask), {dta:.1f} s"}
+                               f"threads (every CPU of the affinity mask), {dta:.1f} s{capped}"}
     L.ur3o_set_threads(threads)
     try:
         others = cpu_other_configs(L, threads)

@@ -218,6 +218,17 @@ int ur3e_batch_queue_stats(ur3e_batch_t* b, unsigned long long* stats);
    static first units, so every one of them is claimed and run by its consumer */
 int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int leave_static_units);
 
+/* multi-GPU (north_star config C4), for hosts that hold their own RCCL communicator (ncclComm_t passed
+   as void*; ur3e_amd/csrc/ur3e_gather.cpp, librccl loaded on first use): after a step, every rank sends
+   its (obs [n, obs_dim], reward [n], terminated [n], truncated [n]) to `root`, which receives all ranks'
+   in rank order into d_*_all ([nranks * n] rows; other ranks pass NULL).  Every rank's handle has the
+   same n; the shards are contiguous global env ids (env_id_offset = rank * n).  Enqueued on `stream` as
+   one point-to-point group, after the step that filled the buffers.  The env path itself has no
+   collective. */
+int ur3e_batch_gather(ur3e_batch_t* b, void* rccl_comm, int root, const double* d_obs, const double* d_reward,
+                      const uint8_t* d_terminated, const uint8_t* d_truncated, double* d_obs_all,
+                      double* d_reward_all, uint8_t* d_terminated_all, uint8_t* d_truncated_all, void* stream);
+
 /* diagnostic (the queue's forward-progress test): launch `workgroups` workgroups on `stream` that each
    hold 64 KB of LDS (two per CU leave room for one step workgroup) for hold_us microseconds, and
    return once they have all started (started = how many had, waited for at most 2 * hold_us), so

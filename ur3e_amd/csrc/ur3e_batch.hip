@@ -388,7 +388,7 @@ struct KState {
   double* sensordata; /* [env][UR3E_MAXSENSORDATA] mjData.sensordata of the last forward (sensors on) */
   double* actfrc; /* [env][UR3E_MAXU] mjData.actuator_force of the last forward (workgroup-per-env kernels) */
   /* tier routing (grasp tier on): hint[e] = the env's last committed forward had more than
-     W_ROUTE_NCON contacts; route[e] = the snapshot of hint the current step routes by (written only
+     KConfig.route_ncon contacts (or route_nefc rows); route[e] = the snapshot of hint the current step routes by (written only
      between steps, by the last kernel of the step): routed envs skip the compact tier and run in the
      grasp tier concurrently with it.  Routing only picks the tier; every tier gives the same result. */
   unsigned char* hint;
@@ -397,10 +397,10 @@ struct KState {
      workgroup, read by the host without a sync to decide whether the next steps need the pre-pass) */
   int* routed_host;
 };
-/* an env whose last forward had more contacts or constraint rows than these runs its next step in
-   the grasp tier (the compact tier holds W_SMALL_MAXCON contacts / W_SMALL_MAXEFC rows; the margin
-   covers a contact or three joint-limit rows one step can add) */
-#define W_ROUTE_NCON (W_SMALL_MAXCON - 1)
+/* an env whose last forward had more contacts or constraint rows than KConfig.route_ncon / route_nefc
+   runs its next step in the grasp tier; the margin below the compact tier's capacity covers what one step
+   can add: a contact or three joint-limit rows for the gym tier (KSS_NV), two contacts or eight rows for
+   the scripted pick's wider tier (KSS_NV_W) */
 /* host-side routing decision (ur3e_batch_step): run-ahead bound and how long routing stays on after
    the host last saw a routed env */
 #define W_AHEAD 16
@@ -408,7 +408,6 @@ struct KState {
 #define W_ROUTE_HOLD 64
 /* grasp-tier workgroups for the compact tier's bails while routing is off (bails are rare then) */
 #define W_GRASP_IDLE_GRID 128
-#define W_ROUTE_NEFC (W_SMALL_MAXEFC - 3)
 
 struct KConfig {
   int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
@@ -421,6 +420,9 @@ struct KConfig {
   int sensors;   /* compute and store mjData.sensordata every forward (full-capacity kernels) */
   unsigned int spin_limit; /* substep queue: flag polls before a waiting unit gives up (diagnostic knob) */
   int leave_static;        /* substep queue diagnostic: owners skip their static units (consumers claim them) */
+  /* routing: an env whose committed forward had more contacts or rows than these runs its next step in
+     the grasp tier (set at create from the handle's compact-tier capacity) */
+  int route_ncon, route_nefc;
   KGains gains;
 };
 
@@ -957,7 +959,7 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   const int od = k_obs_dim(TASK);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
-    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > W_ROUTE_NCON || s.nefc > W_ROUTE_NEFC);
+    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > c.route_ncon || s.nefc > c.route_nefc);
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
     if (stepped && k_is_gym(TASK)) {
       if (rew_out) rew_out[e] = o.r;
@@ -1715,6 +1717,7 @@ struct ur3e_batch {
   int wave_nt; /* 0: lane-per-env kernels (v1); 64/128: workgroup-per-env kernels (v2) */
   int tiered;  /* 1: compact tier (KSS, 64 lanes) + full-capacity fallback over the overflow list */
   int main_tree; /* the model's dof tree equals gen_main_tree.h: use the specialised compact kernel */
+  int wide;      /* the scripted pick's compact tier (KSS_NV_W: 10 contacts / 44 rows) */
   int mesh;      /* the mesh-capable tier set (KSS_NV_M / KSG_NV_M / KSL_M): main.xml's tree with convex
                     meshes, or a model beyond K_NG geoms / W_MAXCAND candidate pairs */
   int* d_ovf_list;
@@ -1935,6 +1938,10 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.sensors = cfg->sensors != 0;
   c.spin_limit = 0;
   c.leave_static = 0;
+  /* the scripted pick (TRAJ_L) on main.xml runs the wider compact tier (KSS_NV_W) */
+  b->wide = tiered && main_tree && !mesh && cfg->task == UR3E_TASK_TRAJ_L;
+  c.route_ncon = b->wide ? W_WIDE_MAXCON - 2 : W_SMALL_MAXCON - 1;
+  c.route_nefc = b->wide ? W_WIDE_MAXEFC - 8 : W_SMALL_MAXEFC - 3;
   for (int k = 0; k < 12; k++) {
     c.gains.task[k] = cfg->task_gains[k];
     c.gains.joint[k] = cfg->joint_gains[k];
@@ -2117,7 +2124,7 @@ extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* 
 /* the tiered step's launches for one tier set (compact KSC, grasp KSG, full capacity KSF): the grasp
    pre-pass (pre), the compact tier, the grasp tier over the compact tier's bails, the full-capacity tier
    over the grasp tier's (or, without the grasp tier, the compact tier's) */
-template <class KSC, class KSG, class KSF>
+template <class KSC, class KSG, class KSF, class KSW>
 static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool pre, const double* d_actions, int adim,
                         double* d_obs, double* d_reward, uint8_t* d_terminated, uint8_t* d_truncated,
                         double* d_terminal_obs) {
@@ -2167,7 +2174,7 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
                        b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                        d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
   } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
-    hipLaunchKernelGGL((w_env_step<64, KSC, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model,
+    hipLaunchKernelGGL((w_env_step<64, KSW, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), w_dyn_lds<KSW>(), st, b->d_model,
                        b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                        d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
   } else if (b->main_tree)
@@ -2240,9 +2247,9 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
       pre = capturing || (b->last_route >= 0 && b->hstep - b->last_route < W_ROUTE_HOLD);
       if (!pre) kst.route = nullptr;
     }
-    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M, KSS_NV_M>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                       d_terminated, d_truncated, d_terminal_obs)
-                           : launch_tiers<KSS_NV, KSG_NV, KSL>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+                           : launch_tiers<KSS_NV, KSG_NV, KSL, KSS_NV_W>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                 d_terminated, d_truncated, d_terminal_obs);
     if (rc != UR3E_OK) return rc;
   } else if (b->wave_nt == 128 && b->mesh)
@@ -2437,8 +2444,9 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
       dyn = w_dyn_lds<KSS_NV_M>();
     } else {
       fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
-                     : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
-      dyn = b->main_tree ? w_dyn_lds<KSS_NV>() : w_dyn_lds<KSS>();
+           : b->wide ? (const void*)w_env_step<64, KSS_NV_W, UR3E_TASK_TRAJ_L>
+           : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
+      dyn = b->wide ? w_dyn_lds<KSS_NV_W>() : b->main_tree ? w_dyn_lds<KSS_NV>() : w_dyn_lds<KSS>();
     }
   } else if (b->wave_nt == 128) {
     nt = 128;

@@ -301,6 +301,16 @@ typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC> KSS;
 /* compact tier specialised for main.xml: compile-time dof count and dof tree (gen_main_tree.h),
    so dof loops have constant trip counts and tree tests fold away */
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1> KSS_NV;
+/* the compact tier of the scripted pick (move_l_mug, TRAJ_L): its approach and release rows see 5-8
+   contacts, which the gym tier would route to the grasp tier (measured: C3 5.9 M env-steps/s at 5/30
+   against 8.0 M at 10/44; the gym workload the other way round, 8.07 M against 7.84 M) */
+#ifndef W_WIDE_MAXCON
+#define W_WIDE_MAXCON 10
+#endif
+#ifndef W_WIDE_MAXEFC
+#define W_WIDE_MAXEFC 44
+#endif
+typedef KSX<W_WIDE_MAXCON, W_WIDE_MAXEFC, UR3E_MAIN_NV, 1> KSS_NV_W;
 static_assert(UR3E_MAIN_NV <= K_NV, "main.xml dofs exceed K_NV");
 /* grasp tier, between the compact and the full-capacity tier: the compact tier's code path (overlaid
    LDS layout, register-resident solver with two rows per lane) sized for a firm grasp of the
