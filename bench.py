@@ -380,6 +380,9 @@ def main():
     ap.add_argument("--cpu-sample-steps", type=int, default=1000)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C3 secondary throughput numbers")
+    ap.add_argument("--queue-split", type=int, default=None,
+                    help="A/B knob: percent of each unit queue's envs whose last substep runs as two half units "
+                         "(default: the library's)")
     ap.add_argument("--pre-steps", type=int, default=500,
                     help="untimed env-steps after reset, so the timed window is mid-episode (contact regime)")
     ap.add_argument("--gather-self", action="store_true",
@@ -422,6 +425,8 @@ def main():
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=1234,
                          env_id_offset=rank * n, envs_per_block=args.envs_per_block)
     batch = rt.Batch(mc, cfg, n, device=local)
+    if args.queue_split is not None:
+        batch.set_queue_split(args.queue_split)
     batch_kinfo = batch.kernel_info()
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
@@ -577,6 +582,7 @@ def main():
                                             -64: "full-capacity, 64 lanes per env"}.get(
                            batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),
                        "kernel_resources": batch_kinfo,
+                       "queue_split_percent": args.queue_split if args.queue_split is not None else "library default",
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
             "window": {"pre_steps_untimed": args.pre_steps,

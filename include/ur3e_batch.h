@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define UR3E_ABI_VERSION 8
+#define UR3E_ABI_VERSION 9
 
 /* tasks (what one env-step means) */
 #define UR3E_TASK_GYM_V2 0  /* action [N,4] task-space (x,y,z,grip): gym ur3e-v2 */
@@ -200,11 +200,12 @@ int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream);
 /* env-steps the compact tier handed on to the fallback tiers since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 
-/* since create (synchronises): counts[0] env-steps the compact tier handed on to the grasp tier,
-   counts[1] env-steps the grasp tier handed on to the full-capacity tier, counts[2] env-steps routed
-   straight to the grasp tier (the env's previous forward had more than 8 contacts or 36 constraint
-   rows; it runs on an
-   internal stream concurrently with the compact tier) */
+/* since create (synchronises): counts[0] env-steps the compact tier handed on (to the grasp tier while
+   routing is in use, else straight to the full-capacity tier), counts[1] env-steps that reached the
+   full-capacity tier, counts[2] env-steps routed straight to the grasp tier (the env's previous forward
+   had more contacts or constraint rows than the compact tier's routing thresholds, 4 / 27 for the gym
+   tasks and 8 / 36 for the scripted pick; it runs on an internal stream concurrently with the compact
+   tier) */
 int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
 
 /* substep work queue (schedule 1), since create (synchronises): stats[0] units that gave up waiting
@@ -217,6 +218,12 @@ int ur3e_batch_queue_stats(ur3e_batch_t* b, unsigned long long* stats);
    waiting unit gives up (0 = the built-in bound, 2^26); leave_static_units = 1: workgroups skip their
    static first units, so every one of them is claimed and run by its consumer */
 int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int leave_static_units);
+
+/* substep work queue (schedule 1): the last `percent` % of each unit queue's envs run their last substep
+   as two half units (the first stops where the forward pass reaches the constraint solver and hands the
+   env's working set to the second, queued after every other unit), so the units that end the launch
+   are shorter.  Results never change.  Default 50; 0 = off.  Non-queued handles accept only 0. */
+int ur3e_batch_set_queue_split(ur3e_batch_t* b, int percent);
 
 /* multi-GPU (north_star config C4), for hosts that hold their own RCCL communicator (ncclComm_t passed
    as void*; ur3e_amd/csrc/ur3e_gather.cpp, librccl loaded on first use): after a step, every rank sends

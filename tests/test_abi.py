@@ -28,7 +28,7 @@ def test_library_exports_header_symbols():
     missing = [s for s in decl if s not in exported]
     assert not missing, missing
     L = ctypes.CDLL(lib)
-    assert L.ur3e_abi_version() == 8
+    assert L.ur3e_abi_version() == 9
     for s in decl:
         getattr(L, s)
 

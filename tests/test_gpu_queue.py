@@ -13,6 +13,10 @@
   which recompute the env-step -- bit-exact against the oracle, and the give-ups are counted.
 - The queue-trace build (unit stamps stored by lane 0 inside the queue kernel's loop) runs at 4,096
   envs bit-exact against the product library and stamps every unit.
+- Split last substeps (ur3e_batch_set_queue_split): with none, half and all of each queue's envs running
+  their last substep as two half units (the working set handed between workgroups through HBM), the
+  results are bit-exact against the oracle, auto-resets inside the resumed halves included; the trace
+  build stamps the second halves too.
 """
 import ctypes
 import os
@@ -186,10 +190,12 @@ def test_trace_build_queue_4096_bit_exact():
     gp = rt.Batch(mc, cfg, n)
     gt = rt.Batch(mc, cfg, n, lib=_build.TRACE_LIB)
     assert gt.kernel_info()["kernel"].startswith("w_env_step_q")
+    gp.set_queue_split(0)
+    gt.set_queue_split(100)  # every env's last substep in two halves: rows 2n.. hold the second halves
     gen = torch.Generator(device="cuda").manual_seed(3)
     lo = torch.tensor(LO, device="cuda")
     hi = torch.tensor(HI, device="cuda")
-    nrow = 2 * n
+    nrow = 3 * n
     tr = np.zeros((nrow, 4), dtype=np.uint64)
     for t in range(steps):
         a = lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda", generator=gen)
@@ -206,5 +212,48 @@ def test_trace_build_queue_4096_bit_exact():
     print("units stamped:", done.mean(), "tier counts:", gt.tier_counts())
     assert done.mean() > 0.9, done.mean()
     assert (finished[done] >= acquired[done]).all() and (acquired[done] >= pulled[done]).all()
+    # a second half starts after its first half has finished (the hand-off flag), on any workgroup
+    both = done[n:2 * n] & done[2 * n:]
+    assert both.mean() > 0.9, both.mean()
+    assert (acquired[2 * n:][both] >= finished[n:2 * n][both]).all()
     gp.close()
     gt.close()
+
+
+def test_queue_split_units_bit_exact():
+    torch = _torch()
+    from oracle import pyoracle as po
+    from ur3e_amd import runtime as rt
+    md, mc = rt.load_model("main")
+    n, steps = 4096, 12
+    # short episodes: the auto-reset runs inside resumed second halves
+    cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=23, max_episode_steps=7)
+    gs = []
+    for pct in (0, 50, 100):
+        g = rt.Batch(mc, cfg, n)
+        assert g.kernel_info()["kernel"].startswith("w_env_step_q")
+        g.set_queue_split(pct)
+        gs.append(g)
+    with pytest.raises(RuntimeError):
+        gs[0].set_queue_split(101)
+    ob = po.OracleBatch(mc, po.config_from(cfg), n)
+    rng = np.random.default_rng(29)
+    for t in range(steps):
+        a = rng.uniform(LO, HI, size=(n, 4))
+        o = ob.step(a)
+        at = torch.from_numpy(a)
+        for g in gs:
+            g.step(at)
+        torch.cuda.synchronize()
+        for pct, g in zip((0, 50, 100), gs):
+            assert np.array_equal(g.obs.cpu().numpy(), o[0]), f"split {pct}: obs step {t}"
+            assert np.array_equal(g.reward.cpu().numpy(), o[1]), f"split {pct}: reward step {t}"
+            assert np.array_equal(g.terminated.cpu().numpy(), o[2]), f"split {pct}: terminated step {t}"
+            assert np.array_equal(g.truncated.cpu().numpy(), o[3]), f"split {pct}: truncated step {t}"
+    oqp, oqv, owa, _ = ob.get_state()
+    for pct, g in zip((0, 50, 100), gs):
+        qp, qv, wa = g.get_state()
+        assert np.array_equal(qp.cpu().numpy(), oqp) and np.array_equal(qv.cpu().numpy(), oqv), f"split {pct}"
+        assert np.array_equal(wa.cpu().numpy(), owa), f"split {pct}"
+        assert g.queue_stats()[0] == 0
+        g.close()

@@ -25,6 +25,9 @@ if __name__ == "__main__":
     fs = 2
     md, mc = rt.load_model("main")
     b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=fs, model=md, seed=1, schedule=sched), n)
+    split = int(os.environ.get("UR3E_SPLIT", "-1"))  # percent of each queue's envs split (default: the library's)
+    if split >= 0:
+        b.set_queue_split(split)
     print('batch created', flush=True)
     L = rt.load_library()
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")
@@ -33,8 +36,9 @@ if __name__ == "__main__":
         b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
         torch.cuda.synchronize()
         print("warm-up step", i, flush=True)
-    nu = n * fs
-    nrow = 8192 + 2048  # units, then one row per workgroup (start, exit)
+    # unit rows sub * n + e, the split units' second halves at fs * n + e; workgroup rows from 12288
+    nu = n * (fs + 1)
+    nrow = 12288 + 2048
     if product:
         print("product library: warm-up steps ran", flush=True)
         sys.exit(0)
@@ -65,8 +69,10 @@ if __name__ == "__main__":
         last_end = np.array(last_end)
         r = dict(step=i, units=int(ok.sum()), slots=slots, span_us=round(float(span), 1),
                  ideal_span_us=round(float(run[ok].sum() / slots), 1),
-                 run_mean_us={int(k): round(float(run[ok & (sub == k)].mean()), 1) for k in range(fs)},
-                 run_p99_us={int(k): round(float(np.percentile(run[ok & (sub == k)], 99)), 1) for k in range(fs)},
+                 run_mean_us={int(k): round(float(run[ok & (sub == k)].mean()), 1) for k in range(fs + 1)
+                              if (ok & (sub == k)).any()},
+                 run_p99_us={int(k): round(float(np.percentile(run[ok & (sub == k)], 99)), 1)
+                             for k in range(fs + 1) if (ok & (sub == k)).any()},
                  wait_total_us_per_slot=round(float(wait[ok].sum() / slots), 2),
                  wait_units_gt_1us=int((wait[ok] > 1.0).sum()),
                  gap_mean_us=round(float(np.mean(gaps)), 2) if gaps else None,

@@ -71,7 +71,7 @@ KD void k_quat_from_matrix(const double mt[9], double q[4]) {
   q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
 
-KD void k_quat_from_rotvec(const double rv[3], double q[4]) {
+__host__ __device__ static inline void k_quat_from_rotvec(const double rv[3], double q[4]) {
   double ang = sqrt(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
   double sc;
   if (ang <= 1e-3) {
@@ -99,10 +99,10 @@ KD void k_rotvec_from_quat(const double qin[4], double rv[3]) {
   rv[0] = sc * q[0]; rv[1] = sc * q[1]; rv[2] = sc * q[2];
 }
 
-KD void k_rot_err(const double xmat[9], const double target[3], double err[3]) {
-  double q[4], qd[4], qi[4], r[4];
+/* the rotation error against a target given as its quaternion qd (k_quat_from_rotvec of the target) */
+KD void k_rot_err_q(const double xmat[9], const double qd[4], double err[3]) {
+  double q[4], qi[4], r[4];
   k_quat_from_matrix(xmat, q);
-  k_quat_from_rotvec(target, qd);
   qi[0] = -q[0]; qi[1] = -q[1]; qi[2] = -q[2]; qi[3] = q[3];
   double cr[3];
   k_cross3(cr, qd, qi);
@@ -111,6 +111,12 @@ KD void k_rot_err(const double xmat[9], const double target[3], double err[3]) {
   r[2] = qd[3] * qi[2] + qi[3] * qd[2] + cr[2];
   r[3] = qd[3] * qi[3] - qd[0] * qi[0] - qd[1] * qi[1] - qd[2] * qi[2];
   k_rotvec_from_quat(r, err);
+}
+
+KD void k_rot_err(const double xmat[9], const double target[3], double err[3]) {
+  double qd[4];
+  k_quat_from_rotvec(target, qd);
+  k_rot_err_q(xmat, qd, err);
 }
 
 /* ================================================================== */
@@ -406,8 +412,6 @@ struct KState {
 #define W_AHEAD 16
 #define W_NTOTAL 5 /* device counters of ur3e_batch::d_ovf_total */
 #define W_ROUTE_HOLD 64
-/* grasp-tier workgroups for the compact tier's bails while routing is off (bails are rare then) */
-#define W_GRASP_IDLE_GRID 128
 
 struct KConfig {
   int task, frame_skip, max_episode_steps, auto_reset, reset_noise, reset_key;
@@ -420,6 +424,10 @@ struct KConfig {
   int sensors;   /* compute and store mjData.sensordata every forward (full-capacity kernels) */
   unsigned int spin_limit; /* substep queue: flag polls before a waiting unit gives up (diagnostic knob) */
   int leave_static;        /* substep queue diagnostic: owners skip their static units (consumers claim them) */
+  double gym_qd[4];        /* the gym tasks' fixed tcp rotation target (rotvec [-1.209, -1.209, 1.209]) as a
+                              quaternion, k_quat_from_rotvec on the host (detmath: the same bits) */
+  int split_from;          /* substep queue: envs of a queue from this index on run their last substep as two
+                              half units (w_env_step_q); >= the envs per queue: no split */
   /* routing: an env whose committed forward had more contacts or rows than these runs its next step in
      the grasp tier (set at create from the handle's compact-tier capacity) */
   int route_ncon, route_nefc;
@@ -883,10 +891,10 @@ struct WOut {
 
 /* The compact tier's working set (the overlaid layout, with WOut behind it) lives in DYNAMIC LDS, sized
    at launch (w_dyn_lds): with static LDS the compiler derives the kernel's occupancy from it -- 16 KB
-   allows 10 workgroups per CU, i.e. 2.5 waves per SIMD, which it rounds down to 2 and then keeps 206
-   registers, so no SIMD would take a third wave.  Out of its sight, the kernel is compiled for three
-   waves per SIMD (168 registers, W_COMPACT_WPE) and the hardware places ten envs per CU.  The other
-   layouts keep static LDS. */
+   allows 10 workgroups per CU, i.e. 2.5 waves per SIMD, which it rounds down to 2.  Out of its sight,
+   the waves per SIMD the kernel is compiled for are W_COMPACT_WPE's alone (2, ~205 registers: eight envs
+   per CU; 3 builds the measured-slower 168-register, ten-per-CU variant).  The other layouts keep
+   static LDS. */
 template <class KS>
 constexpr size_t w_wout_off() { return (sizeof(KS) + 15) & ~(size_t)15; }
 /* W_DYN_PAD: diagnostic builds only (A/B of the register budget at a fixed occupancy): extra dynamic
@@ -1075,16 +1083,89 @@ WD void w_store_mid(KModel m, double* __restrict__ mid, int e, const KS& s) {
    W_DONE (results staged for w_commit), W_BAIL (the compact tier overflowed: nothing was written)
    or W_PAUSED (sub_end < frame_skip: the state after substep sub_end - 1 is in LDS for
    w_store_mid).  sub_begin > 0 resumes from the mid-step state `mid`, skipping the controller. */
+/* UR3eEnv2's epilogue (obs, compute_reward, termination, the success bonus; the lane-0 branch of
+   w_env_step_body) with its five square roots on lanes 0-4 and its four exponentials (tanh's included)
+   on lanes 0-3, one pass each instead of one after the other on lane 0: every operand and expression is
+   k_reward_v2's / w_termination_v2's, so the bits are the same.  One wavefront (64 lanes). */
+template <class KS>
+WD void w_epilogue_v2_lanes(KModel m, const KConfig& c, const KS& s, WOut& o, int cfl) {
+  constexpr int NT = 64;
+  const int tid = w_lane();
+  const int t = o.t + 1;
+  if (tid == 0) {
+    o.t = t;
+    w_obs_v2(m, s, o.obs, cfl);
+  }
+  SYNC();
+  const double* ob = o.obs;
+  /* lane 0: |g2m.xy|, 1: |m2t|, 2: |gripper velocity|, 3: |tcp - mug| (termination), 4: |mug - target|
+     (success); the two-term sum gets + 0 * 0, an exact no-op on a sum of squares */
+  const int k = tid < 5 ? tid : 0;
+  double v0, v1, v2;
+  if (k == 0) { v0 = ob[9]; v1 = ob[10]; v2 = 0.0; }
+  else if (k == 1) { v0 = ob[12]; v1 = ob[13]; v2 = ob[14]; }
+  else if (k == 2) { v0 = ob[15]; v1 = ob[16]; v2 = ob[17]; }
+  else if (k == 3) { v0 = ob[0] - ob[3]; v1 = ob[1] - ob[4]; v2 = ob[2] - ob[5]; }
+  else { v0 = ob[3] - ob[6]; v1 = ob[4] - ob[7]; v2 = ob[5] - ob[8]; }
+  const double nrm = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+  const double xy = rl(nrm, 0), place = rl(nrm, 1), gvn = rl(nrm, 2), dterm = rl(nrm, 3), dsucc = rl(nrm, 4);
+  const double mug_z = ob[5], zerr = fabs(ob[11] - 0.02);
+  const double tx = 8.0 * (mug_z > 0 ? mug_z : 0); /* ur3e_tanh's argument; its |x| is x (>= 0 or NaN) */
+  const double ax = tx < 0 ? -tx : tx;
+  const int j = tid < 4 ? tid : 0;
+  const double arg = j == 0 ? -10 * xy : (j == 1 ? -20 * zerr : (j == 2 ? -15 * place : 2.0 * ax));
+  const double ex = ur3e_exp(arg);
+  const double e_xy = rl(ex, 0), e_z = rl(ex, 1), e_pl = rl(ex, 2), e_th = rl(ex, 3);
+  if (tid == 0) {
+    const double grasped = ob[23], grip = o.a[3];
+    const double ready = e_xy * e_z;
+    const double align = 2.0 * ready;
+    const double grasp_act = 2.0 * grip * ready;
+    const double grasp_ach = 10.0 * grasped * ready;
+    const double th_t = ax > 22.0 ? 1.0 : 1.0 - 2.0 / (e_th + 1.0);
+    const double lift = 8.0 * grasped * (tx < 0 ? -th_t : th_t);
+    const double placement = grasped * (4.0 * e_pl - 1.5 * place);
+    double success = 0.0;
+    if (grasped != 0 && place < 0.05) success = 50.0;
+    double pen = 0.0;
+    pen += -1.0 * (-ob[11] > 0 ? -ob[11] : 0);
+    pen += -0.01 * gvn;
+    double r = align + grasp_act + grasp_ach + lift + placement + success + pen;
+    int term = 1.0 < dterm ? 1 : ((cfl >> 2) & 1 ? 1 : ob[5] <= m->fish_topple_z);
+    const int trunc = c.max_episode_steps > 0 ? (t >= c.max_episode_steps) : 0;
+    if (dsucc < 0.05) {
+      term = 1;
+      r += 50.0;
+    }
+    o.ep_return += r;
+    o.ep_len += 1;
+    o.r = r;
+    o.term = term;
+    o.trunc = trunc;
+  }
+}
+
+/* the gym tasks' controller and epilogue spread over lanes (1, default) or on lane 0 (0: A/B) */
+#ifndef W_EPI_LANES
+#define W_EPI_LANES 1
+#endif
 #define W_BAIL 0
 #define W_DONE 1
 #define W_PAUSED 2
+#define W_HALF 3
+/* half (the queue's split last substep, compact tier): 0 = whole substeps; 1 = run until the first
+   forward pass of the last substep has reached the constraint solver and return W_HALF (the working set
+   in LDS is then handed on whole); 2 = resume there: the caller has restored that working set and WOut,
+   so nothing is loaded and the step goes on with the solver, sub_begin = the last substep */
 template <int NT, int TK = -1, class KS>
 WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c, const KState& st, int e,
                        const double* __restrict__ actions, int adim, KS& s, WOut& o, int sub_begin = 0,
-                       int sub_end = 1 << 30, const double* __restrict__ mid = nullptr) {
+                       int sub_end = 1 << 30, const double* __restrict__ mid = nullptr, int half = 0) {
   const int TASK = TK >= 0 ? TK : c.task; /* TK >= 0: kernel specialised for one task at compile time */
   const int tid = w_lane();
   WT_START();
+  const int fs = (k_is_gym(TASK) || TASK == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  if (half != 2) {
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
   for (int k = tid; k < NCARRY; k += NT) s.carry[k] = st.carry[SC(st, k, e)];
@@ -1118,7 +1199,43 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     SYNC();
   }
   WT(24);
-  if (tid == 0 && sub_begin == 0) {
+#if W_EPI_LANES
+  /* the gym tasks' pid_task_ctrl across lanes: lane r < 6 forms row r of J qdot, of u and column r of
+     J' u (the same sums in the same order as k_pid_task_ctrl); lane 0 alone the rotation error, against
+     the fixed target's quaternion from the host (KConfig.gym_qd) */
+  constexpr bool CTRL_LANES = TK == UR3E_TASK_GYM_V2 || TK == UR3E_TASK_GYM_V0 || TK == UR3E_TASK_IMIT_INDIRECT;
+#else
+  constexpr bool CTRL_LANES = false;
+#endif
+  if constexpr (CTRL_LANES) {
+    if (sub_begin == 0) {
+      const double* J = s.carry + 12;
+      double er = 0;
+      if (tid == 0) {
+        double e3[3];
+        k_rot_err_q(s.carry + 3, c.gym_qd, e3);
+        er = e3[0];
+        s.ctrl[0] = e3[1]; /* staged: the rotation error's y and z for lanes 4 and 5 (ctrl is rewritten below) */
+        s.ctrl[1] = e3[2];
+      }
+      SYNC();
+      const int r = tid < 6 ? tid : 0;
+      double jv = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) jv += J[6 * r + k] * s.qvel[k];
+      const double er_r = r == 3 ? rl(er, 0) : (r == 4 ? s.ctrl[0] : s.ctrl[1]);
+      const double ep_r = o.a[r < 3 ? r : 0] - s.carry[r < 3 ? r : 0];
+      const double u = r < 3 ? c.gains.task[r] * ep_r - c.gains.task[3 + r] * jv
+                             : c.gains.task[6 + r - 3] * er_r - c.gains.task[9 + r - 3] * jv;
+      double su = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) su += J[6 * k + r] * rl(u, k);
+      const double cv = su + s.carry[48 + r];
+      SYNC();
+      if (tid < 6) s.ctrl[tid] = cv;
+      if (tid == 6 && m->nu > 6) s.ctrl[6] = o.a[3] * m->act_ctrlrange[m->nu - 1][1];
+    }
+  } else if (tid == 0 && sub_begin == 0) {
     double ctrl[K_NU];
     if (TASK == UR3E_TASK_GYM_V2 || TASK == UR3E_TASK_TRAJ_L || TASK == UR3E_TASK_GYM_V0 ||
         TASK == UR3E_TASK_IMIT_INDIRECT) {
@@ -1161,10 +1278,11 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   }
   SYNC();
   WT(35);
-  const int fs = (k_is_gym(TASK) || TASK == UR3E_TASK_CTRL) ? c.frame_skip : 1;
+  }
   /* substeps, the bad-qacc retry and the auto-reset all go through ONE w_forward site */
   int sub = sub_begin, retried = 0, resetting = 0;
-  w_step_pre<NT>(m, s);
+  int part = half == 2 ? 2 : 0; /* the resumed unit's first forward pass starts at the solver */
+  if (half != 2) w_step_pre<NT>(m, s);
   for (;;) {
     /* the model and plan are read-only kernel arguments, so their loads are invariant and LICM
        would hoist every model constant of the forward pass out of this loop, keeping them live
@@ -1183,8 +1301,12 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     const KPlan* pli = (const KPlan*)plg;
 #define m mi
 #define pl pli
-    w_forward<NT>(m, pl, s);
+    /* the split unit stops in the first forward pass of the last substep */
+    const int p = (half == 1 && sub == fs - 1 && !retried && !resetting) ? 1 : part;
+    part = 0;
+    w_forward<NT>(m, pl, s, p);
     if (KS::BAIL && s.ovf) return W_BAIL;
+    if (p == 1) return W_HALF;
     if (resetting) {
       w_reset_finish<NT, TK>(m, pl, c, s, o);
       return W_DONE;
@@ -1231,7 +1353,14 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       o.trunc = trunc;
     }
     const int cfl = TASK == UR3E_TASK_GYM_V2 ? w_contact_flags<NT>(m, s) : 0;
-    if (tid == 0 && TASK == UR3E_TASK_GYM_V2) {
+#if W_EPI_LANES
+    constexpr bool EPI_LANES = TK == UR3E_TASK_GYM_V2 && NT == 64;
+#else
+    constexpr bool EPI_LANES = false;
+#endif
+    if constexpr (EPI_LANES) {
+      w_epilogue_v2_lanes(m, c, s, o, cfl);
+    } else if (tid == 0 && TASK == UR3E_TASK_GYM_V2) {
       int t = o.t + 1;
       o.t = t;
       w_obs_v2(m, s, o.obs, cfl);
@@ -1296,6 +1425,9 @@ __global__ __launch_bounds__(NT) void w_env_reset(const ur3e_model_t* __restrict
    s_memrealtime (100 MHz) at start and end, XCC_ID:HW_ID, and did_reset | ncon << 8 | blockIdx << 32 */
 #ifdef UR3E_WAVE_TRACE
 #define UR3E_WAVE_TRACE_MAX 16384
+/* the queue kernel's rows: units at sub * n + e (the split units' second halves at frame_skip * n + e),
+   then one row per workgroup from W_TRACE_WG_ROW */
+#define W_TRACE_WG_ROW 12288
 __device__ unsigned long long ur3e_wave_trace[UR3E_WAVE_TRACE_MAX][4];
 /* which lanes store the queue kernel's unit stamps: every lane (same word, same value; default) or
    lane 0 alone (-DUR3E_TRACE_LANE0) */
@@ -1378,12 +1510,56 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_st
    running; so every wait ends while only resident workgroups make progress.  The spin stays
    bounded (KConfig.spin_limit polls): a unit that gives up claims the env for the fallback tiers
    (atomic exchange: exactly one appender), which recompute the env-step from the committed state,
-   and counts the give-up (queue_stats[0]). */
+   and counts the give-up (queue_stats[0]).
+   Split last substep (KConfig.split_from < envs per queue, half_buf set): the launch's last units are
+   shortened.  For the envs of a queue from split_from on, the last substep's unit stops where its first
+   forward pass reaches the constraint solver and hands the env's whole working set (the dynamic LDS
+   block: KS and WOut) to half_buf (flag epoch << 4 | W_FLAG_HALF); a second-half unit, queued after
+   every other unit, restores it and finishes the substep.  The units that end the launch are then about
+   half a substep long, so the workgroups finish closer together; the hand-off is a copy of the LDS
+   bytes, so the results are unchanged. */
+#define W_FLAG_HALF 13
+#ifndef W_SPLIT_PERCENT
+#define W_SPLIT_PERCENT 50
+#endif
 #define W_FLAG_CLAIMED 14
 #define W_FLAG_BAILED 15
 #define W_SPIN_LIMIT (1u << 26)
 #define W_NQUEUE 8 /* one unit queue per XCD (workgroup b serves queue b % 8: speed only) */
 KD int w_flag_poll(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+/* the split unit's hand-off record: the dynamic LDS block (working set, then WOut) in 16-byte words */
+template <class KS>
+constexpr int w_half_words() { return (int)((w_wout_off<KS>() + sizeof(WOut) + 15) / 16); }
+typedef __attribute__((ext_vector_type(4))) unsigned int w_u32x4_t;
+/* write-through (sc1) 16-byte stores of the whole block, drained before the caller's flag release (the
+   same publish recipe as w_store_mid) */
+template <class KS>
+WD void w_store_half(double* __restrict__ half_buf, int e) {
+  extern __shared__ __align__(16) char w_dyn[];
+  constexpr int HW = w_half_words<KS>();
+  const int tid = w_lane();
+  char* p = (char*)half_buf + (size_t)e * HW * 16;
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, HW * 16, 0x00020000);
+  const w_u32x4_t* src = (const w_u32x4_t*)w_dyn;
+#pragma unroll 4
+  for (int i = tid; i < HW; i += 64) __builtin_amdgcn_raw_buffer_store_b128(src[i], rsrc, 16 * i, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+/* sc1 loads of the record back into the dynamic LDS block (after the flag was acquired) */
+template <class KS>
+WD void w_load_half(const double* __restrict__ half_buf, int e) {
+  extern __shared__ __align__(16) char w_dyn[];
+  constexpr int HW = w_half_words<KS>();
+  const int tid = w_lane();
+  const char* p = (const char*)half_buf + (size_t)e * HW * 16;
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, HW * 16, 0x00020000);
+  w_u32x4_t* dst = (w_u32x4_t*)w_dyn;
+#pragma unroll 4
+  for (int i = tid; i < HW; i += 64) dst[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * i, 0, 16);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_model_t* __restrict__ m,
@@ -1396,7 +1572,8 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
                                                                   double* __restrict__ tobs_out, int* __restrict__ ovf_list,
                                                                   int* ovf_ctl, int* qctl, int* flags,
                                                                   double* __restrict__ mid,
-                                                                  unsigned long long* qstats) {
+                                                                  unsigned long long* qstats,
+                                                                  double* __restrict__ half_buf) {
   KS& s = w_smem<KS>();
   WOut& o = w_wout<KS>();
   __shared__ int s_u, s_epoch, s_flag, s_from;
@@ -1406,7 +1583,11 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
   const int nq = (n & 7) ? 1 : W_NQUEUE;
   const int q = (int)blockIdx.x % nq;
   const int nper = n / nq;
-  const int total = nper * fs;
+  /* split last substep for the queue's envs [k0, nper): their second halves are queued last */
+  const int k0 = (half_buf && fs >= 2 && fs <= W_FLAG_HALF - 1 && c.split_from < nper)
+                     ? (c.split_from > 0 ? c.split_from : 0) : nper;
+  const int nfull = nper * fs;
+  const int total = nfull + (nper - k0);
   /* static first units per queue: substep-0 units only */
   const int nstat = min((int)gridDim.x / nq, nper);
   const unsigned int spin_limit = c.spin_limit ? c.spin_limit : W_SPIN_LIMIT;
@@ -1417,8 +1598,8 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
   const int E = __builtin_amdgcn_readfirstlane(s_epoch);
   const int bailed = (E << 4) | W_FLAG_BAILED;
 #ifdef UR3E_WAVE_TRACE
-  /* per workgroup (row 8192 + blockIdx): started, exited */
-  if (8192 + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[8192 + blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+  /* per workgroup (row W_TRACE_WG_ROW + blockIdx): started, exited */
+  if (W_TRACE_WG_ROW + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[W_TRACE_WG_ROW + blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
 #endif
   /* the first unit of every workgroup is static (its rank in its queue; the counters start at the
      number of workgroups per queue): 2,048 workgroups contending for eight counters at once cost
@@ -1436,8 +1617,18 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       u = __builtin_amdgcn_readfirstlane(s_u);
     }
     if (u >= total) break;
-    const int sub = u / nper;
-    const int e0 = q * nper + (u - sub * nper);
+    /* kind: 0 = whole substep unit(s), 1 = first half of the last substep, 2 = its second half */
+    int sub, loc, kind;
+    if (u < nfull) {
+      sub = u / nper;
+      loc = u - sub * nper;
+      kind = (sub == fs - 1 && loc >= k0) ? 1 : 0;
+    } else {
+      sub = fs;
+      loc = k0 + (u - nfull);
+      kind = 2;
+    }
+    const int e0 = q * nper + loc;
     if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
@@ -1459,7 +1650,7 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       if (!__builtin_amdgcn_readfirstlane(s_flag)) continue;
     } else if (sub > 0) {
       if (tid == 0) {
-        const int want = (E << 4) | sub;
+        const int want = (E << 4) | (kind == 2 ? W_FLAG_HALF : sub);
         int f = w_flag_poll(flags + e0);
         int fr = sub;
         /* producer is a static substep-0 unit not claimed yet: claim it and run both substeps */
@@ -1506,17 +1697,31 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
 #ifdef UR3E_WAVE_TRACE
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int r0 = w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, from, sub + 1, mid);
+    if (kind == 2) {
+      w_load_half<KS>(half_buf, e0);
+      SYNC();
+    }
+    const int r0 = kind == 2 ? w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, fs - 1, 1 << 30,
+                                                        nullptr, 2)
+                             : w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, from,
+                                                        kind ? fs : sub + 1, mid, kind);
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const int e = __builtin_amdgcn_readfirstlane(o.e); /* = e0, reloaded from LDS (see WOut::e) */
     if (r == W_BAIL) {
       if (tid == 0) {
         /* the full-capacity tier recomputes the whole env-step from the committed state */
-        const int old = sub + 1 < fs ? atomicExch(flags + e, bailed) : 0;
+        const int old = (sub + 1 < fs || kind == 1) ? atomicExch(flags + e, bailed) : 0;
         if (old != bailed) {
           const int slot = atomicAdd(ovf_ctl, 1);
           if (slot < n) ovf_list[slot] = e;
         }
+      }
+    } else if (r == W_HALF) {
+      w_store_half<KS>(half_buf, e);
+      SYNC();
+      if (tid == 0) {
+        const int old = atomicExch(flags + e, (E << 4) | W_FLAG_HALF);
+        if (old == bailed) atomicExch(flags + e, bailed); /* a consumer gave up and claimed the env */
       }
     } else if (r == W_PAUSED) {
       w_store_mid<NT>(m, mid, e, s);
@@ -1540,7 +1745,7 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
 #endif
   }
 #ifdef UR3E_WAVE_TRACE
-  if (8192 + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[8192 + blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+  if (W_TRACE_WG_ROW + (int)blockIdx.x < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[W_TRACE_WG_ROW + blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
 #endif
   if (tid == 0) {
     __threadfence();
@@ -1571,7 +1776,8 @@ __global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __r
                                                           const int* __restrict__ ovf_list, int* ovf_ctl,
                                                           unsigned long long* __restrict__ ovf_total,
                                                           int* __restrict__ next_list, int* next_ctl,
-                                                          int* __restrict__ pred_list, int* pred_ctl) {
+                                                          int* __restrict__ pred_list, int* pred_ctl,
+                                                          unsigned long long* __restrict__ ovf_total2 = nullptr) {
   __shared__ KS s;
   __shared__ WOut o;
   __shared__ int s_cnt;
@@ -1617,6 +1823,7 @@ __global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __r
       atomicExch(ovf_ctl, 0);
       atomicExch(ovf_ctl + 1, 0);
       if (cnt) atomicAdd(ovf_total, (unsigned long long)cnt);
+      if (cnt && ovf_total2) atomicAdd(ovf_total2, (unsigned long long)cnt); /* the list came from the compact tier */
     }
   }
   SYNC();
@@ -1744,6 +1951,7 @@ struct ur3e_batch {
   int* d_qctl;     /* {next unit per queue [W_NQUEUE], workgroups done, epoch} */
   int* d_flags;    /* [n] per-env substep hand-off flags */
   double* d_mid;   /* [n][W_MID] mid-step state */
+  double* d_half;  /* [n][w_half_words] the split units' working-set hand-off (queue) */
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
@@ -1938,6 +2146,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   c.sensors = cfg->sensors != 0;
   c.spin_limit = 0;
   c.leave_static = 0;
+  c.split_from = 1 << 30;
+  {
+    const double rv[3] = {-1.209, -1.209, 1.209};
+    k_quat_from_rotvec(rv, c.gym_qd);
+  }
   /* the scripted pick (TRAJ_L) on main.xml runs the wider compact tier (KSS_NV_W) */
   b->wide = tiered && main_tree && !mesh && cfg->task == UR3E_TASK_TRAJ_L;
   c.route_ncon = b->wide ? W_WIDE_MAXCON - 2 : W_SMALL_MAXCON - 1;
@@ -2026,7 +2239,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
      (cfg->schedule 1 keeps one workgroup per env-step) */
   b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 &&
               c.frame_skip < W_FLAG_CLAIMED && cfg->schedule != 1; /* flag codes: substeps done < 14 */
-  b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->q_grid = 0;
+  b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->d_half = nullptr; b->q_grid = 0;
   if (b->queued) {
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -2057,6 +2270,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMalloc(&b->d_flags, sizeof(int) * nd));
     HIPCHK(hipMemset(b->d_flags, 0, sizeof(int) * nd));
     HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
+    const size_t hw = (size_t)(b->mesh ? w_half_words<KSS_NV_M>() : w_half_words<KSS_NV>());
+    HIPCHK(hipMalloc(&b->d_half, 16 * hw * nd));
+    /* the last W_SPLIT_PERCENT % of each queue's envs run their last substep as two half units */
+    const int nper = n_envs / nq;
+    b->cfg.split_from = nper - nper * W_SPLIT_PERCENT / 100;
   }
   HIPCHK(hipMemset(b->d_ovf_total, 0, W_NTOTAL * sizeof(unsigned long long)));
   HIPCHK(hipEventCreate(&b->ev0));
@@ -2094,6 +2312,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   }
   if (b->d_flags) (void)hipFree(b->d_flags);
   if (b->d_mid) (void)hipFree(b->d_mid);
+  if (b->d_half) (void)hipFree(b->d_half);
   (void)hipEventDestroy(b->ev0);
   (void)hipEventDestroy(b->ev1);
   delete b;
@@ -2129,6 +2348,12 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
                         double* d_obs, double* d_reward, uint8_t* d_terminated, uint8_t* d_truncated,
                         double* d_terminal_obs) {
   const int task = b->cfg.task;
+  /* routing off (no pre-pass): the grasp tier is not launched at all -- the compact tier's rare bails
+     go straight to the full-capacity tier, which every env fits, and the step is two launches instead
+     of three (an empty grasp-tier launch cost ~1.4 % of the step) */
+  const bool direct = b->grasp && !pre;
+  int* const c_list = direct ? b->d_ovf2_list : b->d_ovf_list;
+  int* const c_ctl = direct ? b->d_ovf2_ctl : b->d_ovf_ctl;
   if (pre) {
     /* fork: envs routed by the last step's hints run in the grasp tier on the side stream while
        the compact tier (which skips them) runs here */
@@ -2137,7 +2362,7 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
     hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
                        b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                        b->d_pred_list, b->d_pred_ctl, b->d_ovf_total + 2, b->d_ovf2_list, b->d_ovf2_ctl,
-                       nullptr, nullptr);
+                       nullptr, nullptr, nullptr);
     HIPCHK(hipEventRecord(b->ev_join, b->side));
   }
   /* main.xml: dof count and tree specialised at compile time; the gym ur3e-v2 and scripted
@@ -2147,62 +2372,64 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
     if (b->queued && task == UR3E_TASK_GYM_V2)
       hipLaunchKernelGGL((w_env_step_q<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st,
                          b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
-                         d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
-                         b->d_mid, b->d_ovf_total + 3);
+                         d_truncated, d_terminal_obs, c_list, c_ctl, b->d_qctl, b->d_flags,
+                         b->d_mid, b->d_ovf_total + 3, b->d_half);
     else if (b->queued)
       hipLaunchKernelGGL((w_env_step_q<64, KSC>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan,
                          b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
-                         b->d_ovf_total + 3);
+                         d_terminal_obs, c_list, c_ctl, b->d_qctl, b->d_flags, b->d_mid,
+                         b->d_ovf_total + 3, b->d_half);
     else
       hipLaunchKernelGGL((w_env_step<64, KSC>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan, b->cfg,
                          kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                         b->d_ovf_list, b->d_ovf_ctl);
+                         c_list, c_ctl);
   } else if (b->queued) { /* substep work queue (w_env_step_q) */
     if (task == UR3E_TASK_GYM_V2)
       hipLaunchKernelGGL((w_env_step_q<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st,
                          b->d_model, b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated,
-                         d_truncated, d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags,
-                         b->d_mid, b->d_ovf_total + 3);
+                         d_truncated, d_terminal_obs, c_list, c_ctl, b->d_qctl, b->d_flags,
+                         b->d_mid, b->d_ovf_total + 3, b->d_half);
     else
       hipLaunchKernelGGL((w_env_step_q<64, KSC>), dim3(b->q_grid), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan,
                          b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                         d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl, b->d_qctl, b->d_flags, b->d_mid,
-                         b->d_ovf_total + 3);
+                         d_terminal_obs, c_list, c_ctl, b->d_qctl, b->d_flags, b->d_mid,
+                         b->d_ovf_total + 3, b->d_half);
   } else if (b->main_tree && task == UR3E_TASK_GYM_V2) {
     hipLaunchKernelGGL((w_env_step<64, KSC, UR3E_TASK_GYM_V2>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model,
                        b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                       d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+                       d_terminal_obs, c_list, c_ctl);
   } else if (b->main_tree && task == UR3E_TASK_TRAJ_L) {
     hipLaunchKernelGGL((w_env_step<64, KSW, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), w_dyn_lds<KSW>(), st, b->d_model,
                        b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
-                       d_terminal_obs, b->d_ovf_list, b->d_ovf_ctl);
+                       d_terminal_obs, c_list, c_ctl);
   } else if (b->main_tree)
     hipLaunchKernelGGL((w_env_step<64, KSC>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan, b->cfg,
                        kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                       b->d_ovf_list, b->d_ovf_ctl);
+                       c_list, c_ctl);
   else
     hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), w_dyn_lds<KSS>(), st, b->d_model, b->d_plan, b->cfg, kst,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
                        b->d_ovf_ctl);
   int grid = b->n < 512 ? b->n : 512;
   if (b->grasp) {
-    if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
-    /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier, whose
-       workgroup 0 also snapshots the routing hints for the next step */
-    const int post_grid = pre || b->g_grid < W_GRASP_IDLE_GRID ? b->g_grid : W_GRASP_IDLE_GRID;
-    hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(post_grid), dim3(64), 0, st, b->d_model, b->d_plan,
-                       b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
-                       nullptr);
+    if (pre) {
+      HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
+      /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier */
+      hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
+                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
+                         nullptr, nullptr);
+    }
+    /* the full-capacity tier, whose workgroup 0 also snapshots the routing hints for the next step;
+       fed by the compact tier directly (routing off), its count is the compact tier's hand-on too */
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                        b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
-                       b->d_pred_ctl);
+                       b->d_pred_ctl, direct ? b->d_ovf_total : nullptr);
   } else {
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr);
+                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr, nullptr);
   }
   return UR3E_OK;
 }
@@ -2230,8 +2457,8 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
     /* the grasp-tier pre-pass runs only while routing is in use: the last route snapshot the host can
        see (host-mapped, read without a sync, possibly a step or two old) routed some env, or the step
        is being captured (a graph replays without the host).  Skipped, the compact tier steps every
-       env (routing is off for this step: route = null), and the few that exceed it bail to the grasp
-       tier after it -- the same results either way, routing only moves work between tiers. */
+       env (routing is off for this step: route = null), and the few that exceed it bail straight to the
+       full-capacity tier after it -- the same results either way, routing only moves work between tiers. */
     KState kst = b->st;
     bool pre = false;
     if (b->grasp) {
@@ -2537,6 +2764,15 @@ extern "C" int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_lim
   if (!b) return fail(UR3E_EINVAL, "null handle");
   b->cfg.spin_limit = spin_limit;
   b->cfg.leave_static = leave_static_units != 0;
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_set_queue_split(ur3e_batch_t* b, int percent) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  if (percent < 0 || percent > 100) return fail(UR3E_EINVAL, "split percent outside [0, 100]");
+  if (!b->queued) return percent ? fail(UR3E_EINVAL, "the handle does not run the substep work queue") : UR3E_OK;
+  const int nper = b->n / ((b->n & 7) ? 1 : W_NQUEUE);
+  b->cfg.split_from = nper - nper * percent / 100;
   return UR3E_OK;
 }
 

@@ -2048,11 +2048,17 @@ WD void w_sensors(KModel m, const KPlan* __restrict__ pl, KS& s) {
 }
 
 /* ================================================================== */
+/* part (compact tier, the queue's split units): 0 = the whole forward pass; 1 = up to the smooth
+   acceleration (everything before the constraint solver), 2 = the rest, from the state part 1 left in
+   LDS.  Part 1's last stage and part 2's first read and write only the working set, so a part-1 unit
+   can hand the working set to another workgroup, which runs part 2 with the same bits. */
 template <int NT, class KS>
-WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
+WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::OVERLAY); /* compact tier: ur3e_wave_r.h */
+  if (REG && part == 2) goto solve;
+  {
   /* diagnostic builds only (-DUR3E_DOUBLE_STAGE=k): the compact tier runs idempotent stage k twice, so
      the difference of SQ_INSTS_VALU against the normal build is that stage's instruction count
      (tools/stage_insts.py); results are unchanged */
@@ -2118,6 +2124,9 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s) {
     w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
   }
   WT(8);
+  if (REG && part == 1) return;
+  }
+solve:
   if constexpr (REG)
     W_DBL(15, r_solve_newton(m, s));
   else

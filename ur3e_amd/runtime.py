@@ -86,6 +86,7 @@ def _bind(L):
     L.ur3e_batch_set_timing.argtypes = [vp, ip]
     L.ur3e_batch_overflow_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_tier_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ur3e_batch_set_queue_split.argtypes = [vp, ctypes.c_int]
     L.ur3e_batch_get_touch.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_carry.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_ctrl.argtypes = [vp, vp, vp]
@@ -343,8 +344,9 @@ class Batch:
         return out[:, :self.model_c.ntouch]
 
     def tier_counts(self) -> tuple:
-        """Since create: (env-steps the compact tier handed to the grasp tier, env-steps the grasp tier
-        handed to the full-capacity tier, env-steps routed straight to the grasp tier)."""
+        """Since create: (env-steps the compact tier handed on -- to the grasp tier while routing is in
+        use, else straight to the full-capacity tier --, env-steps that reached the full-capacity tier,
+        env-steps routed straight to the grasp tier)."""
         v = (ctypes.c_ulonglong * 3)()
         self._chk(self.L.ur3e_batch_tier_counts(self.h, v))
         return int(v[0]), int(v[1]), int(v[2])
@@ -355,6 +357,11 @@ class Batch:
         v = (ctypes.c_ulonglong * 2)()
         self._chk(self.L.ur3e_batch_queue_stats(self.h, v))
         return int(v[0]), int(v[1])
+
+    def set_queue_split(self, percent: int):
+        """Substep work queue: the last `percent` % of each queue's envs run their last substep as two half
+        units (include/ur3e_batch.h: ur3e_batch_set_queue_split); results never change."""
+        self._chk(self.L.ur3e_batch_set_queue_split(self.h, int(percent)))
 
     def set_queue_debug(self, spin_limit: int = 0, leave_static_units: bool = False):
         """Diagnostics of the substep queue: flag polls before a waiting unit gives up (0 = built-in
