@@ -13,7 +13,7 @@ for v in "$@"; do
   W=/tmp/ur3e_var_$v; rm -rf $W; mkdir -p $W; cp -r $R/ur3e_amd $R/include $W/
   if [ -f $R/tools/var/$v.patch ]; then (cd $W && patch -s -p1 < $R/tools/var/$v.patch) || { echo "patch $v failed"; exit 1; }; fi
   XF=""; if [ -f $R/tools/var/$v.flags ]; then XF=$(cat $R/tools/var/$v.flags); fi
-  timeout -k 10 600 /opt/rocm/bin/hipcc $FL $XF -o $W/lib.so $W/ur3e_amd/csrc/ur3e_batch.hip $W/ur3e_amd/csrc/ur3e_vecnorm.hip $W/ur3e_amd/csrc/ur3e_mjcf.cpp -ldl > $D/${v}_build.log 2>&1 &
+  timeout -k 10 600 /opt/rocm/bin/hipcc $FL $XF -o $W/lib.so $W/ur3e_amd/csrc/ur3e_batch.hip $W/ur3e_amd/csrc/ur3e_vecnorm.hip $W/ur3e_amd/csrc/ur3e_mjcf.cpp $W/ur3e_amd/csrc/ur3e_gather.cpp -ldl > $D/${v}_build.log 2>&1 &
   pids="$pids $!"
 done
 for p in $pids; do wait $p || { echo "a variant build failed"; tail -5 $D/*_build.log; exit 1; }; done

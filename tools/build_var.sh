@@ -4,4 +4,4 @@
 set -e
 cd "$(dirname "$0")/.."
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mllvm -disable-machine-licm \
-  -Wno-unused-result "$@" -o ur3e_amd/_lib/libur3e_amd_${VAR:-var}.so ur3e_amd/csrc/ur3e_batch.hip ur3e_amd/csrc/ur3e_vecnorm.hip ur3e_amd/csrc/ur3e_mjcf.cpp -ldl
+  -Wno-unused-result "$@" -o ur3e_amd/_lib/libur3e_amd_${VAR:-var}.so ur3e_amd/csrc/ur3e_batch.hip ur3e_amd/csrc/ur3e_vecnorm.hip ur3e_amd/csrc/ur3e_mjcf.cpp ur3e_amd/csrc/ur3e_gather.cpp -ldl

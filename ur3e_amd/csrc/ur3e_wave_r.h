@@ -92,19 +92,26 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
   }
 }
 
+/* the cone terms' divisions skipped while no contact of the wave is in the cone's middle zone (1,
+   default) or always computed (0: A/B) */
+#ifndef W_CONE_SKIP
+#define W_CONE_SKIP 1
+#endif
 /* mj_constraintUpdate per row (w_constraint_update) */
 template <int RPL>
 WD void r_constraint_update(RRow (&W)[RPL]) {
   const int lane = w_lane();
   double jarv[RPL], f0v[RPL], f1v[RPL], f2v[RPL], Fmv[RPL];
+  double Nv[RPL], Tv[RPL], U1v[RPL], U2v[RPL];
   int zv[RPL];
+  bool anycone = false;
 #pragma unroll
   for (int h = 0; h < RPL; h++) jarv[h] = W[h].jar;
 #pragma unroll
   for (int h = 0; h < RPL; h++) {
     const RRow& w = W[h];
     const int row = lane + 64 * h;
-    const double jar = w.jar, D = w.D;
+    const double jar = w.jar;
     /* contact cone: computed on every lane (uniform shuffles), used by contact lanes */
     double jar1 = shfr(jarv, row + 1), jar2 = shfr(jarv, row + 2);
     double mu = w.mu;
@@ -118,13 +125,29 @@ WD void r_constraint_update(RRow (&W)[RPL]) {
     if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
     else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
     else z = 2;
-    double Dm = D / (mu * mu * (1 + mu * mu));
-    double NT_ = N - mu * T;
-    Fmv[h] = 0.5 * Dm * NT_ * NT_;
-    f0v[h] = -Dm * NT_ * mu;
-    f1v[h] = Dm * NT_ * mu * U1 / T * w.fr0;
-    f2v[h] = Dm * NT_ * mu * U2 / T * w.fr1;
     zv[h] = z;
+    Nv[h] = N; Tv[h] = T; U1v[h] = U1; U2v[h] = U2;
+    const int t = w.typ;
+    anycone |= t >= 0 && t != CN_EQUALITY && t != CN_FRICTION_DOF && t != CN_LIMIT_JOINT && w.jj == 0 && z == 2;
+  }
+  /* the cone force and cost are read only by the rows of a contact whose first row is in the cone's
+     middle zone: with none in the wave (the usual case: sticking or separating contacts), their
+     divisions are skipped (the values are then unused, so every result is unchanged) */
+  if (!W_CONE_SKIP || w_any<64>(anycone)) {
+#pragma unroll
+    for (int h = 0; h < RPL; h++) {
+      const RRow& w = W[h];
+      const double D = w.D, mu = w.mu, N = Nv[h], T = Tv[h], U1 = U1v[h], U2 = U2v[h];
+      double Dm = D / (mu * mu * (1 + mu * mu));
+      double NT_ = N - mu * T;
+      Fmv[h] = 0.5 * Dm * NT_ * NT_;
+      f0v[h] = -Dm * NT_ * mu;
+      f1v[h] = Dm * NT_ * mu * U1 / T * w.fr0;
+      f2v[h] = Dm * NT_ * mu * U2 / T * w.fr1;
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < RPL; h++) { Fmv[h] = 0.0; f0v[h] = 0.0; f1v[h] = 0.0; f2v[h] = 0.0; }
   }
   /* one code path for every row kind (selects, no per-kind branches): the quadratic terms are formed
      once with the expressions every kind used, the linear friction and cone values beside them */
@@ -727,6 +750,8 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
   constexpr int RPL = KS::RPL;
   int zv[RPL];
   double cFv[RPL], cdFv[RPL], cd2Fv[RPL];
+  double Nv[RPL], Tv[RPL], T2v[RPL], U1v[RPL], U2v[RPL];
+  bool anycone = false;
 #pragma unroll
   for (int h = 0; h < RPL; h++) {
     const RRow& w = W[h];
@@ -734,9 +759,9 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
     /* cone terms from the contact's first row (computed everywhere, used by contact lanes) */
     const double jar1 = c.jar1, jar2 = c.jar2, Jv1 = c.Jv1, Jv2 = c.Jv2;
     double mu = w.mu;
-    double U0 = (w.jar + a * w.Jv) * mu, V0 = c.V0;
-    double U1 = (jar1 + a * Jv1) * w.fr0, V1 = c.V1;
-    double U2 = (jar2 + a * Jv2) * w.fr1, V2 = c.V2;
+    double U0 = (w.jar + a * w.Jv) * mu;
+    double U1 = (jar1 + a * Jv1) * w.fr0;
+    double U2 = (jar2 + a * Jv2) * w.fr1;
     double N = U0;
     double T2 = 0;
     T2 += U1 * U1;
@@ -746,17 +771,34 @@ WD void r_ls_eval(KS& s, const RRow (&W)[KS::RPL], const RLs (&C)[KS::RPL], int 
     if (N >= mu * T || (T <= 0 && N >= 0)) z = 0;
     else if (mu * N + T <= 0 || (T <= 0 && N < 0)) z = 1;
     else z = 2;
-    const double Dm = c.Dm, VV = c.VV;
-    double UV = 0;
-    UV += U1 * V1;
-    UV += U2 * V2;
-    double NT_ = N - mu * T;
-    double dNT = V0 - mu * UV / T;
-    double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
-    cFv[h] = 0.5 * Dm * NT_ * NT_;
-    cdFv[h] = Dm * NT_ * dNT;
-    cd2Fv[h] = Dm * (dNT * dNT + NT_ * d2NT);
     zv[h] = z;
+    Nv[h] = N; Tv[h] = T; T2v[h] = T2; U1v[h] = U1; U2v[h] = U2;
+    const int t = w.typ;
+    anycone |= t >= 0 && t != CN_EQUALITY && t != CN_FRICTION_DOF && t != CN_LIMIT_JOINT && w.jj == 0 && z == 2;
+  }
+  /* the cone terms are read only on the first row of a contact in the middle zone (`cone` below): with
+     none in the wave their divisions are skipped (the values are then unused) */
+  if (!W_CONE_SKIP || w_any<64>(anycone)) {
+#pragma unroll
+    for (int h = 0; h < RPL; h++) {
+      const RRow& w = W[h];
+      const RLs& c = C[h];
+      const double mu = w.mu, N = Nv[h], T = Tv[h], T2 = T2v[h], U1 = U1v[h], U2 = U2v[h];
+      const double V0 = c.V0, V1 = c.V1, V2 = c.V2;
+      const double Dm = c.Dm, VV = c.VV;
+      double UV = 0;
+      UV += U1 * V1;
+      UV += U2 * V2;
+      double NT_ = N - mu * T;
+      double dNT = V0 - mu * UV / T;
+      double d2NT = -mu * (VV * T2 - UV * UV) / (T2 * T);
+      cFv[h] = 0.5 * Dm * NT_ * NT_;
+      cdFv[h] = Dm * NT_ * dNT;
+      cd2Fv[h] = Dm * (dNT * dNT + NT_ * d2NT);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < RPL; h++) { cFv[h] = 0.0; cdFv[h] = 0.0; cd2Fv[h] = 0.0; }
   }
   double Fm[RPL], dFm[RPL], d2Fm[RPL];
 #pragma unroll
