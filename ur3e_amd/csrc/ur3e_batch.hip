@@ -933,8 +933,9 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
   if (tid == 0) {
     s.nwarn = st.nwarn[e];
     s.ovf = 0;
-    /* diagnostic contact cap: > 0 caps the compact tier only (its envs then run in the grasp tier),
-       < 0 caps every bailing tier (compact and grasp: the envs reach the full-capacity tier) */
+    /* diagnostic contact cap: > 0 caps the compact tier only (its envs then run in the grasp tier, which
+       the step then always launches behind it), < 0 caps every bailing tier (compact and grasp: the envs
+       reach the full-capacity tier) */
     const int cap = c.tier_con_cap, capv = cap > 0 ? cap : -cap;
     const bool capped = KS::BAIL && (cap < 0 || (cap > 0 && KS::MAXCON <= W_SMALL_MAXCON));
     s.cap_con = (capped && capv < KS::MAXCON) ? capv : KS::MAXCON;
@@ -2351,7 +2352,8 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
   /* routing off (no pre-pass): the grasp tier is not launched at all -- the compact tier's rare bails
      go straight to the full-capacity tier, which every env fits, and the step is two launches instead
      of three (an empty grasp-tier launch cost ~1.4 % of the step) */
-  const bool direct = b->grasp && !pre;
+  const bool direct = b->grasp && !pre && b->cfg.tier_con_cap <= 0; /* a positive diagnostic cap keeps the
+                                                                        grasp tier behind the compact one */
   int* const c_list = direct ? b->d_ovf2_list : b->d_ovf_list;
   int* const c_ctl = direct ? b->d_ovf2_ctl : b->d_ovf_ctl;
   if (pre) {
