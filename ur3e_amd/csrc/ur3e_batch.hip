@@ -2410,12 +2410,11 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
                        c_list, c_ctl);
   else
     hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), w_dyn_lds<KSS>(), st, b->d_model, b->d_plan, b->cfg, kst,
-                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, b->d_ovf_list,
-                       b->d_ovf_ctl);
+                       d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, c_list, c_ctl);
   int grid = b->n < 512 ? b->n : 512;
   if (b->grasp) {
-    if (pre) {
-      HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
+    if (!direct) {
+      if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
       /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier */
       hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                          b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
