@@ -222,7 +222,8 @@ int ur3e_batch_set_queue_debug(ur3e_batch_t* b, unsigned int spin_limit, int lea
 /* substep work queue (schedule 1): the last `percent` % of each unit queue's envs run their last substep
    as two half units (the first stops where the forward pass reaches the constraint solver and hands the
    env's working set to the second, queued after every other unit), so the units that end the launch
-   are shorter.  Results never change.  Default 50; 0 = off.  Non-queued handles accept only 0. */
+   are shorter.  Results never change.  Default 0 (off: measured slower); non-queued
+   handles accept only 0. */
 int ur3e_batch_set_queue_split(ur3e_batch_t* b, int percent);
 
 /* multi-GPU (north_star config C4), for hosts that hold their own RCCL communicator (ncclComm_t passed

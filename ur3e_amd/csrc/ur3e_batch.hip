@@ -1520,8 +1520,11 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_st
    half a substep long, so the workgroups finish closer together; the hand-off is a copy of the LDS
    bytes, so the results are unchanged. */
 #define W_FLAG_HALF 13
+/* off by default: measured same-box at 4,096 envs, 0 / 25 / 50 / 100 % split gave 7.95 / 7.65 / 7.86 /
+   7.89 M env-steps/s (profiles/r04_e3) -- the hand-off and the second halves' waits on their first halves
+   cost more than the shorter tail returns */
 #ifndef W_SPLIT_PERCENT
-#define W_SPLIT_PERCENT 50
+#define W_SPLIT_PERCENT 0
 #endif
 #define W_FLAG_CLAIMED 14
 #define W_FLAG_BAILED 15
@@ -2273,7 +2276,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
     const size_t hw = (size_t)(b->mesh ? w_half_words<KSS_NV_M>() : w_half_words<KSS_NV>());
     HIPCHK(hipMalloc(&b->d_half, 16 * hw * nd));
-    /* the last W_SPLIT_PERCENT % of each queue's envs run their last substep as two half units */
+    /* the last W_SPLIT_PERCENT % of each queue's envs run their last substep as two half units (0: none) */
     const int nper = n_envs / nq;
     b->cfg.split_from = nper - nper * W_SPLIT_PERCENT / 100;
   }
