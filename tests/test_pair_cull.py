@@ -1,0 +1,86 @@
+"""The compact tier's pre-narrowphase cull (ur3e_amd/csrc/ur3e_wave.h: w_pair_apart), restated in numpy
+and checked against the CPU oracle: over random gym ur3e-v2 states and states pressed against the table,
+every candidate pair the cull removes has no contact in the oracle's contact list (so skipping its
+narrowphase cannot change a result), and the cull removes most of the plane-box pairs that the bounding
+spheres keep.  The GPU side runs the same expressions; its bit-exactness is in the -m gpu parity tests."""
+import ctypes
+
+import numpy as np
+
+from oracle import pyoracle as po
+from ur3e_amd import runtime as rt
+
+PLANE, BOX = 0, 6
+
+
+def _apart(md, xp, xm, p):
+    g1, g2 = md["cpair_geom1"][p], md["cpair_geom2"][p]
+    t1, t2 = md["geom_type"][g1], md["geom_type"][g2]
+    margin = md["cpair_margin"][p]
+    if t2 != BOX:
+        return False
+    size2 = np.asarray(md["geom_size"][g2])
+    if t1 == PLANE:
+        pm, bm = xm[g1], xm[g2]
+        n = np.array([pm[2], pm[5], pm[8]])
+        dist = n @ (xp[g2] - xp[g1])
+        ext = sum(size2[c] * abs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]) for c in range(3))
+        return dist - ext > margin + 1e-9
+    if t1 != BOX:
+        return False
+    size1 = np.asarray(md["geom_size"][g1])
+    a = np.asarray(xm[g1]).reshape(3, 3).T  # a[k] = column k
+    b = np.asarray(xm[g2]).reshape(3, 3).T
+    pp = xp[g2] - xp[g1]
+    for ax in list(a) + list(b):
+        ext = sum(size1[k] * abs(a[k] @ ax) for k in range(3)) + sum(size2[k] * abs(b[k] @ ax) for k in range(3))
+        if abs(pp @ ax) - ext > margin:
+            return True
+    return False
+
+
+def _states(md, mc):
+    n = 32
+    cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=2, max_episode_steps=60)
+    ob = po.OracleBatch(mc, po.config_from(cfg), n)
+    rng = np.random.default_rng(1)
+    lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
+    hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
+    low = np.array([0.29799994, 0.13349916, 0.0, 1.0])
+    out = []
+    for t in range(60):
+        # every other window drives the gripper down onto the mug and table
+        a = rng.uniform(lo, hi, size=(n, 4)) if (t // 15) % 2 == 0 else np.tile(low, (n, 1))
+        ob.step(a)
+        if t % 6 == 5:
+            qp, qv, _, _ = ob.get_state()
+            out.extend(zip(qp, qv))
+    return out
+
+
+def test_culled_pairs_have_no_oracle_contacts():
+    md, mc = rt.load_model("main")
+    L = po.lib()
+    L.ur3o_data_geom_pose.argtypes = [ctypes.c_void_p] * 4
+    ng = md["ngeom"]
+    ncp = len(md["cpair_geom1"])
+    plane_box = [p for p in range(ncp) if md["geom_type"][md["cpair_geom1"][p]] == PLANE
+                 and md["geom_type"][md["cpair_geom2"][p]] == BOX]
+    culled_pb = kept_pb = contacts_seen = 0
+    for qp, qv in _states(md, mc):
+        d = po.OracleData(mc, L=L)
+        d.set(qpos=qp, qvel=qv)
+        d.forward()
+        xp, xm = np.zeros((ng, 3)), np.zeros((ng, 9))
+        L.ur3o_data_geom_pose(ctypes.byref(mc), d.buf, xp.ctypes.data, xm.ctypes.data)
+        touching = {tuple(sorted(g)) for g in d.contacts()["geoms"].tolist()}
+        contacts_seen += len(touching)
+        for p in range(ncp):
+            if _apart(md, xp, xm, p):
+                pair = tuple(sorted((md["cpair_geom1"][p], md["cpair_geom2"][p])))
+                assert pair not in touching, f"pair {p} {pair} culled but in contact"
+                culled_pb += p in plane_box
+            else:
+                kept_pb += p in plane_box
+    assert contacts_seen > 0
+    assert culled_pb > 5 * kept_pb, (culled_pb, kept_pb)

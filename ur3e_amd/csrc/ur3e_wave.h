@@ -775,6 +775,60 @@ WD bool w_pair_near(KModel m, const KS& s, int p) {
   return true;
 }
 
+/* The pair is certain to give no contact, decided before the narrowphase (bounding spheres alone keep every
+   plane pair and the always-overlapping neighbours: 27 of main.xml's 92 candidates survive them in every
+   gym state, 24 of them plane-box).  Plane-box: the box's lowest corner, n.(c - p) - sum_i h_i |n.a_i|,
+   lies beyond the margin by more than 1e-9 -- every corner's computed distance then exceeds the margin
+   too (their rounding error is ~1e-15 of the ~1 m scale), so k_plane_box_t would emit none.  Box-box:
+   the six face axes of k_box_box_t's separating-axis test, computed with the same expressions in the
+   same order, and one of them separates beyond the margin -- the routine returns 0 there.  Either way
+   the pair's result (no contact) is unchanged, and only its narrowphase is skipped. */
+template <class KS>
+WD bool w_pair_apart(KModel m, const KS& s, int p) {
+  const int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
+  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const double margin = m->cpair_margin[p];
+  if (t2 != UR3E_GEOM_BOX) return false;
+  if (t1 == UR3E_GEOM_PLANE) {
+    const double* pm = s.geom_xmat[g1];
+    const double* bm = s.geom_xmat[g2];
+    const double n[3] = {pm[2], pm[5], pm[8]};
+    const double dif[3] = {s.geom_xpos[g2][0] - s.geom_xpos[g1][0], s.geom_xpos[g2][1] - s.geom_xpos[g1][1],
+                           s.geom_xpos[g2][2] - s.geom_xpos[g1][2]};
+    const double dist = k_dot3(n, dif);
+    double ext = 0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) ext += m->geom_size[g2][c] * fabs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]);
+    return dist - ext > margin + 1e-9;
+  }
+  if (t1 != UR3E_GEOM_BOX) return false;
+  const double* R1 = s.geom_xmat[g1];
+  const double* R2 = s.geom_xmat[g2];
+  const double* s1 = m->geom_size[g1];
+  const double* s2 = m->geom_size[g2];
+  double a[3][3], b[3][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    a[k][0] = R1[k]; a[k][1] = R1[3 + k]; a[k][2] = R1[6 + k];
+    b[k][0] = R2[k]; b[k][1] = R2[3 + k]; b[k][2] = R2[6 + k];
+  }
+  const double pp[3] = {s.geom_xpos[g2][0] - s.geom_xpos[g1][0], s.geom_xpos[g2][1] - s.geom_xpos[g1][1],
+                        s.geom_xpos[g2][2] - s.geom_xpos[g1][2]};
+  bool apart = false;
+#pragma unroll
+  for (int code = 0; code < 6; code++) {
+    const double* ax = code < 3 ? a[code] : b[code - 3];
+    double ext = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) ext += s1[k] * fabs(k_dot3(a[k], ax));
+#pragma unroll
+    for (int k = 0; k < 3; k++) ext += s2[k] * fabs(k_dot3(b[k], ax));
+    const double sep = fabs(k_dot3(pp, ax)) - ext;
+    apart |= sep > margin;
+  }
+  return apart;
+}
+
 /* geom g as a convex shape (convex.h): box half sizes, or its mesh's hull vertices (model image) */
 template <class KS>
 __device__ __forceinline__ void w_geom_convex(KModel m, const KS& s, int g, ur3e_cvx* c) {
@@ -932,6 +986,10 @@ WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
    candidate order (ballot + mbcnt), ONE narrowphase per survivor (lane = survivor), contact
    offsets by a wave prefix scan of the counts, contacts written from the lane's own results.
    Same contacts in the same order as the count / prefix / write passes of w_collision. */
+/* the exact pre-narrowphase cull (w_pair_apart) on (1, default) or off (0: A/B) */
+#ifndef W_PAIR_CULL
+#define W_PAIR_CULL 1
+#endif
 template <class KS>
 WD void r_collision(KModel m, KS& s) {
   const int lane = w_lane();
@@ -942,7 +1000,7 @@ WD void r_collision(KModel m, KS& s) {
   constexpr int CAP = KS::OVERLAY ? W_MAXSURV : KS::NCAND;
   for (int base = 0; base < np; base += 64) {
     const int p = base + lane;
-    const bool ok = p < np && w_pair_near(m, s, p);
+    const bool ok = p < np && w_pair_near(m, s, p) && !(W_PAIR_CULL && w_pair_apart(m, s, p));
     const unsigned long long bm = __ballot(ok);
     const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
     if (ok && at < CAP) s.cand_off[at] = p;
