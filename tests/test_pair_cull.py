@@ -1,22 +1,27 @@
 """The compact tier's pre-narrowphase cull (ur3e_amd/csrc/ur3e_wave.h: w_pair_apart), restated in numpy
 and checked against the CPU oracle: over random gym ur3e-v2 states and states pressed against the table,
 every candidate pair the cull removes has no contact in the oracle's contact list (so skipping its
-narrowphase cannot change a result), and the cull removes most of the plane-box pairs that the bounding
-spheres keep.  The GPU side runs the same expressions; its bit-exactness is in the -m gpu parity tests."""
+narrowphase cannot change a result), and the cull removes most of the plane-box (and, on the mesh model,
+plane-mesh) pairs that the bounding spheres keep.  The GPU side runs the same expressions; its bit-exactness is in the -m gpu parity tests."""
 import ctypes
 
 import numpy as np
+import pytest
 
 from oracle import pyoracle as po
 from ur3e_amd import runtime as rt
 
-PLANE, BOX = 0, 6
+PLANE, BOX, MESH = 0, 6, 7
 
 
 def _apart(md, xp, xm, p):
     g1, g2 = md["cpair_geom1"][p], md["cpair_geom2"][p]
     t1, t2 = md["geom_type"][g1], md["geom_type"][g2]
     margin = md["cpair_margin"][p]
+    if t1 == PLANE and t2 == MESH:
+        pm = xm[g1]
+        n = np.array([pm[2], pm[5], pm[8]])
+        return n @ (xp[g2] - xp[g1]) - md["geom_rbound"][g2] > margin + 1e-9
     if t2 != BOX:
         return False
     size2 = np.asarray(md["geom_size"][g2])
@@ -58,14 +63,15 @@ def _states(md, mc):
     return out
 
 
-def test_culled_pairs_have_no_oracle_contacts():
-    md, mc = rt.load_model("main")
+@pytest.mark.parametrize("model", ["main", "main_mesh"])
+def test_culled_pairs_have_no_oracle_contacts(model):
+    md, mc = rt.load_model(model)
     L = po.lib()
     L.ur3o_data_geom_pose.argtypes = [ctypes.c_void_p] * 4
     ng = md["ngeom"]
     ncp = len(md["cpair_geom1"])
     plane_box = [p for p in range(ncp) if md["geom_type"][md["cpair_geom1"][p]] == PLANE
-                 and md["geom_type"][md["cpair_geom2"][p]] == BOX]
+                 and md["geom_type"][md["cpair_geom2"][p]] in (BOX, MESH)]
     culled_pb = kept_pb = contacts_seen = 0
     for qp, qv in _states(md, mc):
         d = po.OracleData(mc, L=L)

@@ -781,13 +781,24 @@ WD bool w_pair_near(KModel m, const KS& s, int p) {
    lies beyond the margin by more than 1e-9 -- every corner's computed distance then exceeds the margin
    too (their rounding error is ~1e-15 of the ~1 m scale), so k_plane_box_t would emit none.  Box-box:
    the six face axes of k_box_box_t's separating-axis test, computed with the same expressions in the
-   same order, and one of them separates beyond the margin -- the routine returns 0 there.  Either way
+   same order, and one of them separates beyond the margin -- the routine returns 0 there.  Plane-mesh:
+   the hull's bounding radius (below).  Either way
    the pair's result (no contact) is unchanged, and only its narrowphase is skipped. */
 template <class KS>
 WD bool w_pair_apart(KModel m, const KS& s, int p) {
   const int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const double margin = m->cpair_margin[p];
+  if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_MESH) {
+    /* every hull vertex lies within geom_rbound of the geom's origin (the compiler's bound over the
+       same vertices), so the centre beyond the margin by more than rbound + 1e-9 keeps every vertex
+       distance of ur3e_plane_convex_clear above the margin: the pair is clear */
+    const double* pm = s.geom_xmat[g1];
+    const double n[3] = {pm[2], pm[5], pm[8]};
+    const double dif[3] = {s.geom_xpos[g2][0] - s.geom_xpos[g1][0], s.geom_xpos[g2][1] - s.geom_xpos[g1][1],
+                           s.geom_xpos[g2][2] - s.geom_xpos[g1][2]};
+    return k_dot3(n, dif) - m->geom_rbound[g2] > margin + 1e-9;
+  }
   if (t2 != UR3E_GEOM_BOX) return false;
   if (t1 == UR3E_GEOM_PLANE) {
     const double* pm = s.geom_xmat[g1];
