@@ -22,24 +22,27 @@ def _apart(md, xp, xm, p):
         pm = xm[g1]
         n = np.array([pm[2], pm[5], pm[8]])
         return n @ (xp[g2] - xp[g1]) - md["geom_rbound"][g2] > margin + 1e-9
-    if t2 != BOX:
+    if t2 not in (BOX, MESH):
         return False
     size2 = np.asarray(md["geom_size"][g2])
     if t1 == PLANE:
+        if t2 == MESH:
+            return False
         pm, bm = xm[g1], xm[g2]
         n = np.array([pm[2], pm[5], pm[8]])
         dist = n @ (xp[g2] - xp[g1])
         ext = sum(size2[c] * abs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]) for c in range(3))
         return dist - ext > margin + 1e-9
-    if t1 != BOX:
+    if t1 not in (BOX, MESH):
         return False
+    lim = margin + 1e-6 if MESH in (t1, t2) else margin  # a hull inside its geom_size box
     size1 = np.asarray(md["geom_size"][g1])
     a = np.asarray(xm[g1]).reshape(3, 3).T  # a[k] = column k
     b = np.asarray(xm[g2]).reshape(3, 3).T
     pp = xp[g2] - xp[g1]
     for ax in list(a) + list(b):
         ext = sum(size1[k] * abs(a[k] @ ax) for k in range(3)) + sum(size2[k] * abs(b[k] @ ax) for k in range(3))
-        if abs(pp @ ax) - ext > margin:
+        if abs(pp @ ax) - ext > lim:
             return True
     return False
 
@@ -90,3 +93,20 @@ def test_culled_pairs_have_no_oracle_contacts(model):
                 kept_pb += p in plane_box
     assert contacts_seen > 0
     assert culled_pb > 5 * kept_pb, (culled_pb, kept_pb)
+
+
+def test_mesh_hulls_inside_their_boxes_and_spheres():
+    """the premise of the plane-mesh and mesh-pair clauses: every hull vertex of the mesh model lies in its
+    geom's geom_size box and within its geom_rbound"""
+    md, _ = rt.load_model("main_mesh")
+    verts = np.asarray(md["mesh_vert"]).reshape(-1, 3)
+    checked = 0
+    for g in range(md["ngeom"]):
+        if md["geom_type"][g] != MESH:
+            continue
+        i = md["geom_dataid"][g]
+        v = verts[md["mesh_vertadr"][i]:md["mesh_vertadr"][i] + md["mesh_vertnum"][i]]
+        assert (np.abs(v) <= np.asarray(md["geom_size"][g]) + 1e-15).all()
+        assert (np.linalg.norm(v, axis=1) <= md["geom_rbound"][g] + 1e-12).all()
+        checked += 1
+    assert checked == 17

@@ -782,7 +782,7 @@ WD bool w_pair_near(KModel m, const KS& s, int p) {
    too (their rounding error is ~1e-15 of the ~1 m scale), so k_plane_box_t would emit none.  Box-box:
    the six face axes of k_box_box_t's separating-axis test, computed with the same expressions in the
    same order, and one of them separates beyond the margin -- the routine returns 0 there.  Plane-mesh:
-   the hull's bounding radius (below).  Either way
+   the hull's bounding radius; box-mesh and mesh-mesh: the hulls' boxes (below).  Either way
    the pair's result (no contact) is unchanged, and only its narrowphase is skipped. */
 template <class KS>
 WD bool w_pair_apart(KModel m, const KS& s, int p) {
@@ -799,8 +799,10 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
                            s.geom_xpos[g2][2] - s.geom_xpos[g1][2]};
     return k_dot3(n, dif) - m->geom_rbound[g2] > margin + 1e-9;
   }
-  if (t2 != UR3E_GEOM_BOX) return false;
+  const bool mesh2 = t2 == UR3E_GEOM_MESH, mesh1 = t1 == UR3E_GEOM_MESH;
+  if (t2 != UR3E_GEOM_BOX && !mesh2) return false;
   if (t1 == UR3E_GEOM_PLANE) {
+    if (mesh2) return false;
     const double* pm = s.geom_xmat[g1];
     const double* bm = s.geom_xmat[g2];
     const double n[3] = {pm[2], pm[5], pm[8]};
@@ -812,7 +814,12 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
     for (int c = 0; c < 3; c++) ext += m->geom_size[g2][c] * fabs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]);
     return dist - ext > margin + 1e-9;
   }
-  if (t1 != UR3E_GEOM_BOX) return false;
+  if (t1 != UR3E_GEOM_BOX && !mesh1) return false;
+  /* box-box: k_box_box_t's own decision (> margin).  A convex mesh lies inside its geom_size box (the
+     compiler's half extents of the same hull vertices), so two shapes whose boxes separate by more than
+     the margin + 1e-6 along a face axis are apart beyond the margin: GJK (ur3e_convex_separated /
+     the full tier's GJK + EPA) finds no contact for them, to well within that 1e-6 */
+  const double lim = (mesh1 || mesh2) ? margin + 1e-6 : margin;
   const double* R1 = s.geom_xmat[g1];
   const double* R2 = s.geom_xmat[g2];
   const double* s1 = m->geom_size[g1];
@@ -835,7 +842,7 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
 #pragma unroll
     for (int k = 0; k < 3; k++) ext += s2[k] * fabs(k_dot3(b[k], ax));
     const double sep = fabs(k_dot3(pp, ax)) - ext;
-    apart |= sep > margin;
+    apart |= sep > lim;
   }
   return apart;
 }
