@@ -1146,6 +1146,10 @@ WD void w_epilogue_v2_lanes(KModel m, const KConfig& c, const KS& s, WOut& o, in
   }
 }
 
+/* touch sensors only in the env-step's last forward pass (1, default) or in every pass (0: A/B) */
+#ifndef W_TOUCH_LAST
+#define W_TOUCH_LAST 1
+#endif
 /* the gym tasks' controller and epilogue spread over lanes (1, default) or on lane 0 (0: A/B) */
 #ifndef W_EPI_LANES
 #define W_EPI_LANES 1
@@ -1305,7 +1309,9 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
     /* the split unit stops in the first forward pass of the last substep */
     const int p = (half == 1 && sub == fs - 1 && !retried && !resetting) ? 1 : part;
     part = 0;
-    w_forward<NT>(m, pl, s, p);
+    /* touch sensors: only the env-step's last forward pass (the last substep's, or the auto-reset's)
+       reaches the commit */
+    w_forward<NT>(m, pl, s, p, W_TOUCH_LAST ? (sub == fs - 1 || resetting) : true);
     if (KS::BAIL && s.ovf) return W_BAIL;
     if (p == 1) return W_HALF;
     if (resetting) {

@@ -2128,8 +2128,10 @@ WD void w_sensors(KModel m, const KPlan* __restrict__ pl, KS& s) {
    acceleration (everything before the constraint solver), 2 = the rest, from the state part 1 left in
    LDS.  Part 1's last stage and part 2's first read and write only the working set, so a part-1 unit
    can hand the working set to another workgroup, which runs part 2 with the same bits. */
+/* touch = false (compact tier): skip the touch sensors -- the caller's later forward pass of the same
+   env-step recomputes them before anything reads them (w_commit reads the last pass's) */
 template <int NT, class KS>
-WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0) {
+WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0, bool touch = true) {
   const int tid = w_lane();
   const int nv = NVOF(KS, m);
   constexpr bool REG = (NT == 64 && KS::OVERLAY); /* compact tier: ur3e_wave_r.h */
@@ -2211,6 +2213,7 @@ solve:
   /* touch sensors, oracle sensor_touch: sum over contacts (in contact order) of the normal force
      of contacts on the sensor's body whose ray hits the site box */
   if constexpr (NT == 64 && KS::MAXCON <= 16) {
+    if (touch) {
     /* lane = (sensor, contact): every contact tested at once, then an ordered per-sensor sum with
        -0.0 (the exact additive identity) for contacts that do not count */
     const int ts = tid >> 4, ci = tid & 15;
@@ -2243,6 +2246,7 @@ solve:
       if (tid == k) mine = sum;
     }
     if (tid < nt) s.touch[tid] = mine;
+    }
     WT(21);
   } else if (tid < m->ntouch) {
     const int site = m->touch_site[tid];
