@@ -1207,8 +1207,10 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
 #if W_EPI_LANES
   /* the gym tasks' pid_task_ctrl across lanes: lane r < 6 forms row r of J qdot, of u and column r of
      J' u (the same sums in the same order as k_pid_task_ctrl); lane 0 alone the rotation error, against
-     the fixed target's quaternion from the host (KConfig.gym_qd) */
-  constexpr bool CTRL_LANES = TK == UR3E_TASK_GYM_V2 || TK == UR3E_TASK_GYM_V0 || TK == UR3E_TASK_IMIT_INDIRECT;
+     the fixed target's quaternion from the host (KConfig.gym_qd) or, for the scripted pick (TRAJ_L), the
+     row's own rotvec target */
+  constexpr bool CTRL_LANES = TK == UR3E_TASK_GYM_V2 || TK == UR3E_TASK_GYM_V0 || TK == UR3E_TASK_IMIT_INDIRECT ||
+                              TK == UR3E_TASK_TRAJ_L;
 #else
   constexpr bool CTRL_LANES = false;
 #endif
@@ -1218,7 +1220,8 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       double er = 0;
       if (tid == 0) {
         double e3[3];
-        k_rot_err_q(s.carry + 3, c.gym_qd, e3);
+        if constexpr (TK == UR3E_TASK_TRAJ_L) k_rot_err(s.carry + 3, o.a + 3, e3); /* the row's rotvec target */
+        else k_rot_err_q(s.carry + 3, c.gym_qd, e3);
         er = e3[0];
         s.ctrl[0] = e3[1]; /* staged: the rotation error's y and z for lanes 4 and 5 (ctrl is rewritten below) */
         s.ctrl[1] = e3[2];
@@ -1238,7 +1241,7 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
       const double cv = su + s.carry[48 + r];
       SYNC();
       if (tid < 6) s.ctrl[tid] = cv;
-      if (tid == 6 && m->nu > 6) s.ctrl[6] = o.a[3] * m->act_ctrlrange[m->nu - 1][1];
+      if (tid == 6 && m->nu > 6) s.ctrl[6] = o.a[TK == UR3E_TASK_TRAJ_L ? 6 : 3] * m->act_ctrlrange[m->nu - 1][1];
     }
   } else if (tid == 0 && sub_begin == 0) {
     double ctrl[K_NU];
