@@ -1529,6 +1529,9 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_st
    half a substep long, so the workgroups finish closer together; the hand-off is a copy of the LDS
    bytes, so the results are unchanged. */
 #define W_FLAG_HALF 13
+#ifndef W_CLAIM_AHEAD
+#define W_CLAIM_AHEAD 1
+#endif
 /* off by default: measured same-box at 4,096 envs, 0 / 25 / 50 / 100 % split gave 7.95 / 7.65 / 7.86 /
    7.89 M env-steps/s (profiles/r04_e3) -- the hand-off and the second halves' waits on their first halves
    cost more than the shorter tail returns */
@@ -1618,12 +1621,22 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
      number of workgroups per queue): 2,048 workgroups contending for eight counters at once cost
      ~10 us of the launch */
   int first = (int)blockIdx.x / nq < nstat;
+  /* the next unit, pulled while the current one runs (W_CLAIM_AHEAD): the pull's round trip overlaps the
+     unit's own state loads instead of standing between two units.  Only while the queue is far from its
+     end (two workgroup-rounds of units left), so the last units are still taken by whichever workgroup
+     frees first.  A unit waits only on units of lower index, and a workgroup's pulled-ahead unit has a
+     higher index than the one it runs, so every chain of waits ends at a running unit. */
+  const int nslot = (int)gridDim.x / nq;
+  int next = -1;
   for (;;) {
     int u;
     const int is_static = first;
     if (first) {
       u = (int)blockIdx.x / nq;
       first = 0;
+    } else if (next >= 0) {
+      u = next;
+      next = -1;
     } else {
       if (tid == 0) s_u = atomicAdd(qctl + q, 1);
       SYNC();
@@ -1714,6 +1727,9 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       w_load_half<KS>(half_buf, e0);
       SYNC();
     }
+    const bool ahead = W_CLAIM_AHEAD && u + 2 * nslot < total;
+    int nxt = 0;
+    if (ahead && tid == 0) nxt = atomicAdd(qctl + q, 1);
     const int r0 = kind == 2 ? w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, fs - 1, 1 << 30,
                                                         nullptr, 2)
                              : w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, from,
@@ -1745,6 +1761,11 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       }
     } else {
       w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+    }
+    if (ahead) {
+      if (tid == 0) s_u = nxt;
+      SYNC();
+      next = __builtin_amdgcn_readfirstlane(s_u);
     }
     SYNC();
 #ifdef UR3E_WAVE_TRACE
