@@ -1146,6 +1146,11 @@ WD void w_epilogue_v2_lanes(KModel m, const KConfig& c, const KS& s, WOut& o, in
   }
 }
 
+/* the resumed unit's mid-step record loaded together with the committed state (1, default) or after it
+   (0: A/B) */
+#ifndef W_MID_EARLY
+#define W_MID_EARLY 1
+#endif
 /* touch sensors only in the env-step's last forward pass (1, default) or in every pass (0: A/B) */
 #ifndef W_TOUCH_LAST
 #define W_TOUCH_LAST 1
@@ -1171,23 +1176,32 @@ WD int w_env_step_body(KModel m, const KPlan* __restrict__ pl, const KConfig& c,
   WT_START();
   const int fs = (k_is_gym(TASK) || TASK == UR3E_TASK_CTRL) ? c.frame_skip : 1;
   if (half != 2) {
+  /* resume (sub_begin > 0): the state after the previous unit's substeps and the ctrl it applied, one
+     16-byte sc1 load per lane (the record's doubles 2 tid, 2 tid + 1).  It is issued before the
+     committed-state loads, so the two round trips overlap, and scattered to LDS after them (it
+     overwrites qpos, qvel, warm start and ctrl) */
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+  u32x4_t wmid = {0u, 0u, 0u, 0u};
+  const double* pmid = mid + (size_t)e * W_MID;
+  if (W_MID_EARLY && sub_begin > 0 && tid < W_MID / 2) {
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)pmid, 0, W_MID * 8, 0x00020000);
+    wmid = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 0, 16);
+  }
   w_load<NT>(m, c, st, e, s, o);
   for (int k = tid; k < adim && k < 8; k += NT) o.a[k] = actions[(size_t)e * adim + k];
   for (int k = tid; k < NCARRY; k += NT) s.carry[k] = st.carry[SC(st, k, e)];
   SYNC();
   if (sub_begin > 0) {
-    /* resume: the state after the previous unit's substeps, and the ctrl it applied */
-    /* one 16-byte sc1 load per lane (the record's doubles 2 tid, 2 tid + 1), scattered to LDS */
-    const double* p = mid + (size_t)e * W_MID;
     if (tid < W_MID / 2) {
-      __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, W_MID * 8, 0x00020000);
-      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
-      const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 0, 16);
+      if (!W_MID_EARLY) {
+        __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)pmid, 0, W_MID * 8, 0x00020000);
+        wmid = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 0, 16);
+      }
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int k = 2 * tid + h;
         const double x = __builtin_bit_cast(
-            double, (unsigned long long)w[2 * h] | ((unsigned long long)w[2 * h + 1] << 32));
+            double, (unsigned long long)wmid[2 * h] | ((unsigned long long)wmid[2 * h + 1] << 32));
         if (k < W_MID_QVEL) {
           if (k < m->nq) s.qpos[k] = x;
         } else if (k < W_MID_WARM) {
