@@ -1146,10 +1146,10 @@ WD void w_epilogue_v2_lanes(KModel m, const KConfig& c, const KS& s, WOut& o, in
   }
 }
 
-/* the resumed unit's mid-step record loaded together with the committed state (1, default) or after it
-   (0: A/B) */
+/* the resumed unit's mid-step record loaded together with the committed state (1) or after it (0) */
+/* off: no measurable difference same-box (profiles/r04_ab A/B 8) */
 #ifndef W_MID_EARLY
-#define W_MID_EARLY 1
+#define W_MID_EARLY 0
 #endif
 /* touch sensors only in the env-step's last forward pass (1, default) or in every pass (0: A/B) */
 #ifndef W_TOUCH_LAST
@@ -1543,8 +1543,10 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_st
    half a substep long, so the workgroups finish closer together; the hand-off is a copy of the LDS
    bytes, so the results are unchanged. */
 #define W_FLAG_HALF 13
+/* off: measured 4.3 % slower same-box (8.02-8.03 against 8.39-8.40 M env-steps/s, profiles/r04_ab A/B 8) --
+   pulled-ahead units are no longer given to whichever workgroup frees first */
 #ifndef W_CLAIM_AHEAD
-#define W_CLAIM_AHEAD 1
+#define W_CLAIM_AHEAD 0
 #endif
 /* off by default: measured same-box at 4,096 envs, 0 / 25 / 50 / 100 % split gave 7.95 / 7.65 / 7.86 /
    7.89 M env-steps/s (profiles/r04_e3) -- the hand-off and the second halves' waits on their first halves
@@ -1635,7 +1637,7 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
      number of workgroups per queue): 2,048 workgroups contending for eight counters at once cost
      ~10 us of the launch */
   int first = (int)blockIdx.x / nq < nstat;
-  /* the next unit, pulled while the current one runs (W_CLAIM_AHEAD): the pull's round trip overlaps the
+  /* the next unit, pulled while the current one runs (W_CLAIM_AHEAD, off by default): the pull's round trip overlaps the
      unit's own state loads instead of standing between two units.  Only while the queue is far from its
      end (two workgroup-rounds of units left), so the last units are still taken by whichever workgroup
      frees first.  A unit waits only on units of lower index, and a workgroup's pulled-ahead unit has a
