@@ -1146,6 +1146,10 @@ WD void w_epilogue_v2_lanes(KModel m, const KConfig& c, const KS& s, WOut& o, in
   }
 }
 
+/* workgroups of the full-capacity tier's launch (grid-stride over its list; it runs empty on most steps) */
+#ifndef W_FULL_GRID
+#define W_FULL_GRID 512
+#endif
 /* the resumed unit's mid-step record loaded together with the committed state (1) or after it (0) */
 /* off: no measurable difference same-box (profiles/r04_ab A/B 8) */
 #ifndef W_MID_EARLY
@@ -2460,7 +2464,7 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
   else
     hipLaunchKernelGGL((w_env_step<64, KSS>), dim3(b->n), dim3(64), w_dyn_lds<KSS>(), st, b->d_model, b->d_plan, b->cfg, kst,
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, c_list, c_ctl);
-  int grid = b->n < 512 ? b->n : 512;
+  int grid = b->n < W_FULL_GRID ? b->n : W_FULL_GRID;
   if (b->grasp) {
     if (!direct) {
       if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
