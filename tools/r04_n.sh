@@ -1,0 +1,9 @@
+#!/bin/bash
+# round-4 GPU call: the GPU suite, then a same-box A/B of the constraint Jacobian's unit-vector rows
+# (mctriv0 = all groups in the shuffle passes), into gpurun_out/$1
+set -o pipefail
+R=$(pwd); D=$R/gpurun_out/$1; mkdir -p $D
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_tests.txt 2>&1
+rc=$?; tail -3 $D/gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.txt 2>&1 || exit $?
+bash tools/ab_multi.sh 3 mctriv0 > $D/ab.txt 2>&1; rc=$?; tail -7 $D/ab.txt; [ $rc -eq 0 ] || exit $rc

@@ -92,6 +92,11 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
   }
 }
 
+/* the constraint Jacobian's unit-vector rows written by readlane, outside the shuffle passes (1, default),
+   or every group in the shuffle passes (0: A/B) */
+#ifndef W_MC_TRIVIAL
+#define W_MC_TRIVIAL 1
+#endif
 /* the cone terms' divisions skipped while no contact of the wave is in the cone's middle zone (1,
    default) or always computed (0: A/B) */
 #ifndef W_CONE_SKIP
@@ -1795,10 +1800,52 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
     double cd[6];
     for (int r = 0; r < 6; r++) cd[r] = s.cdof[vv][r];
     const unsigned int vbit = 1u << vv;
+#if W_MC_TRIVIAL
+    /* the unit-vector rows (joint equality, frictionloss, limit: one row each) one group at a time, with
+       the group's scalars by readlane and every dof lane writing its entry; the shuffle passes below then
+       take only the connect and contact groups, GS at a time in group order */
+    const unsigned long long heavy = __ballot(lane < ngrp && (gtype == G_CONNECT || gtype >= G_CONTACT));
+    {
+      unsigned long long triv = __ballot(lane < ngrp) & ~heavy;
+      while (triv) {
+        const int g = (int)__builtin_ctzll(triv);
+        triv &= triv - 1;
+        const int type = rli(gtype, g), r = rli(grow, g), d1 = rli(dof1, g), d2 = rli(dof2, g);
+        const double dp = rl(dpoly, g), sd = rl(side, g);
+        if (lane < nv) {
+          double val;
+          if (type == G_JOINTEQ) {
+            val = 0;
+            if (lane == d1) val = 1;
+            if (d2 >= 0 && lane == d2) val = -dp;
+          } else if (type == G_FLOSS) {
+            val = lane == d1 ? 1.0 : 0.0;
+          } else {
+            val = lane == d1 ? -sd : 0.0;
+          }
+          s.efc_J[r][lane] = val;
+        }
+      }
+    }
+    const int nheavy = __popcll(heavy);
+    unsigned long long hrest = heavy;
+    for (int g0 = 0; g0 < nheavy; g0 += GS) {
+      /* the groups of heavy ranks g0 .. g0 + GS - 1 (uniform), slot t takes the t-th */
+      int gpick = 0;
+#pragma unroll
+      for (int t = 0; t < GS; t++) {
+        const int gt = hrest ? (int)__builtin_ctzll(hrest) : 0;
+        hrest &= hrest - 1;
+        gpick = slot == t ? gt : gpick;
+      }
+      const bool on = slot < GS && g0 + slot < nheavy && v < nv;
+      const int gs = on ? gpick : 0;
+#else
     for (int g0 = 0; g0 < ngrp; g0 += GS) {
       const int g = g0 + slot;
       const bool on = slot < GS && g < ngrp && v < nv;
       const int gs = on ? g : 0;
+#endif
       const int type = shfi(gtype, gs), r = shfi(grow, gs);
       const unsigned int m1 = (unsigned int)shfi(msk1, gs), m2 = (unsigned int)shfi(msk2, gs);
       const int d1 = shfi(dof1, gs), d2 = shfi(dof2, gs);
