@@ -35,6 +35,14 @@ ALGO_BYTES_PER_ENV_STEP = 1898
 FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
+# the two compiles of the reference's assets/main.xml (ur3e_amd/model/compiler.py): its mesh files are
+# git-ignored upstream, so the headline runs the documented box surrogate; main_mesh has SURVEY §2.3's collision
+# set with synthetic convex stand-in hulls for every mesh file (tools/make_main_meshes.py)
+MODEL_VARIANT = {"main": "model variant: box surrogate for the mesh geoms (15 colliding geoms, 92 candidate pairs)",
+                 "main_mesh": "model variant: convex stand-in hulls for the mesh geoms (24 colliding geoms, 17 meshes, "
+                              "234 candidate pairs)"}
+
+
 def _profile_file(kind: str):
     """profiles/<kind>_rNN.json of the newest round that has one (traffic: PMC HBM bytes per launch of
     the step kernel; flops: the oracle-counted FP64 flops per env-step), or None.  Each file records the
@@ -385,6 +393,9 @@ def main():
                          "(default: the library's)")
     ap.add_argument("--pre-steps", type=int, default=500,
                     help="untimed env-steps after reset, so the timed window is mid-episode (contact regime)")
+    ap.add_argument("--model", default="main", choices=["main", "main_mesh"],
+                    help="main: main.xml's box-surrogate compile (the headline); main_mesh: main.xml with convex "
+                         "stand-in hulls for its mesh files (the reference's collision set)")
     ap.add_argument("--gather-self", action="store_true",
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
     args = ap.parse_args()
@@ -421,7 +432,7 @@ def main():
     torch.cuda.set_device(dev)
 
     n = args.envs_per_gpu
-    md, mc = rt.load_model("main")
+    md, mc = rt.load_model(args.model)
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=1234,
                          env_id_offset=rank * n, envs_per_block=args.envs_per_block)
     batch = rt.Batch(mc, cfg, n, device=local)
@@ -522,7 +533,8 @@ def main():
     if rank == 0:
         achieved = ALGO_BYTES_PER_ENV_STEP * n / (step_kernel_ms * 1e-3) / 1e9
         prof_traffic, traffic_src = None, None
-        tf = _profile_file("traffic")
+        sfx = "" if args.model == "main" else "_mesh"   # profiles of the model variant that ran
+        tf = _profile_file("traffic" + sfx)
         if tf:
             try:
                 with open(tf) as f:
@@ -532,7 +544,7 @@ def main():
             except Exception:
                 prof_traffic = None
         fp64 = None
-        ff = _profile_file("flops")
+        ff = _profile_file("flops" + sfx)
         if ff:
             try:
                 with open(ff) as f:
@@ -546,7 +558,7 @@ def main():
             except Exception:
                 fp64 = None
         cpu, parity = None, None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.model == "main":
             try:
                 cpu, p_gym = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
                 parity = {"gym_v2": p_gym, "move_l_mug": move_l_mug_parity(steps=args.cpu_sample_steps),
@@ -555,7 +567,7 @@ def main():
             except Exception as e:  # the oracle is only the checker; never fail the bench on it
                 cpu = dict(value=None, unit="env-steps/s", cores=None, kind="port", sample=f"failed: {e}")
         extra = None
-        if world == 1 and not args.no_extra:
+        if world == 1 and not args.no_extra and args.model == "main":
             try:
                 extra = other_configs(n_envs=n)
             except Exception as e:  # secondary numbers never fail the headline line
@@ -573,7 +585,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform random actions in the ur3e-v2 action Box, generated into HBM before the timed region; stochastic 'high' mug resets; timed window starts after --pre-steps untimed env-steps, mid-episode)",
-            "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset)",
+            "config": {"workload": "main.xml gym ur3e-v2 step (pid_task_ctrl + 2 substeps + obs/reward/auto-reset), "
+                                   + MODEL_VARIANT[args.model],
                        "envs_per_gpu": n, "global_envs": n * world, "frame_skip": 2,
                        "kernel_layout": {0: f"two-tier: compact 64-lane wavefront per env ({batch_kinfo.get('lds_bytes')} B lifetime-overlaid LDS working set,"
                                                f" {batch_kinfo.get('regs')} VGPRs: {batch_kinfo.get('envs_per_cu')} envs/CU)"

@@ -2,13 +2,15 @@
 hulls for every mesh file it names (tools/make_main_meshes.py -> ur3e_amd/assets/main_mesh.model.json:
 24 colliding geoms, 17 of them convex meshes, 234 candidate pairs) -- bit for bit against the oracle.
 
-It runs in the mesh-capable tier set (KSS_NV_M / KSG_NV_M / KSL_M): the compact and grasp tiers settle a
-mesh pair whose hulls GJK (or, against the table plane, the hull's vertex distances) finds apart beyond
-the margin, and hand on an env-step whose mesh pair may touch to the full-capacity tier, which runs
-GJK + EPA.  Two workloads:
+It runs in the mesh-capable tier set (KSS_NV_M / KSG_NV_M / KSL_M).  The compact and grasp tiers settle
+every mesh pair themselves, one pair per wavefront (ur3e_cvx_wave.h: plane-convex, GJK and EPA with the
+hull vertices across lanes and the simplex / polytope in LDS); the full-capacity tier runs convex.h per
+lane.  Two workloads:
   * gym ur3e-v2 with random actions: no mesh contact, every env-step stays in the compact tier;
   * move_j holding poses where the gripper's linkage meshes rest on the mug and a pad box on the upper
-    arm mesh (contacts box-mesh): those env-steps reach the full-capacity tier."""
+    arm mesh (contacts box-mesh, EPA): with routing (default), with the grasp tier always behind the
+    compact one (tier_con_cap 5: no env-step reaches the full-capacity tier), and with a diagnostic
+    contact cap (tier_con_cap < 0) sending them to the full-capacity tier -- bit-exact every way."""
 import numpy as np
 import pytest
 
@@ -62,14 +64,15 @@ def test_main_mesh_gym_bit_exact_in_the_compact_tier():
     gb.close()
 
 
-def test_main_mesh_contacts_reach_the_full_tier_bit_exact():
+@pytest.mark.parametrize("cap", [0, 5, -1])
+def test_main_mesh_contacts_bit_exact(cap):
     torch = _torch()
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     md, mc = rt.load_model("main_mesh")
     n, steps = 32, 120
     cfg = rt.make_config(task=rt.TASK_MOVE_J, frame_skip=1, model=md, seed=4, reset_noise=False,
-                         reset_key=md["id_key_down"], max_episode_steps=0, auto_reset=False)
+                         reset_key=md["id_key_down"], max_episode_steps=0, auto_reset=False, tier_con_cap=cap)
     gb = rt.Batch(mc, cfg, n)
     ob = po.OracleBatch(mc, po.config_from(cfg), n)
     rng = np.random.default_rng(9)
@@ -101,5 +104,12 @@ def test_main_mesh_contacts_reach_the_full_tier_bit_exact():
     tc = gb.tier_counts()
     print("tier counts (compact->grasp, grasp->full, routed):", tc, "mesh contacts sampled:", mesh_contacts)
     assert mesh_contacts > 0
-    assert tc[1] > 0  # the touching mesh pairs ran GJK + EPA in the full-capacity tier
+    if cap < 0:
+        assert tc[1] > 0  # capped: the touching mesh pairs ran GJK + EPA in the full-capacity tier
+    elif cap > 0:
+        # the grasp tier always behind the compact one (a positive cap): every env-step, touching mesh pairs
+        # included, is settled by the wavefront's convex narrowphase in the compact or the grasp tier
+        assert tc[1] == 0
+    # cap 0 (routing): the compact tier's bails before the host turns routing on (a few steps) go straight to
+    # the full-capacity tier, the rest are routed to the grasp tier
     gb.close()

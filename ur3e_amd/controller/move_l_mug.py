@@ -41,17 +41,19 @@ class MoveLMug:
     """N scripted pick-and-place episodes stepping in lock-step."""
 
     def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
-                 envs_per_block: int = 0, sensors: bool = False, config_yaml_path: str | None = None):
+                 envs_per_block: int = 0, sensors: bool = False, config_yaml_path: str | None = None,
+                 model: str = "main"):
         """sensors=True also keeps the full mjData.sensordata (incl. the torque sensors) readable through
         batch.get_sensordata() after a step, at the cost of the full-capacity kernel (see
         ur3e_config_t.sensors).  The reference's per-row records -- traj_true (get_task_space_state) and
         actuator_frc (get_jnt_torques), move_l_mug.py:80-81 -- need no sensors flag: run(record=True)
-        fills them on the device every row, in every tier."""
+        fills them on the device every row, in every tier.  model="main_mesh" runs main.xml compiled with
+        convex meshes (tools/make_main_meshes.py) in the mesh-capable tier set."""
         import torch
         from .. import gains
         from .. import runtime as rt
         self.torch = torch
-        md, mc = rt.load_model("main")
+        md, mc = rt.load_model(model)
         self.md = md
         # controller/move_l_mug.py:20-26: gains from config_l_mug.yml
         cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,

@@ -76,6 +76,65 @@ struct KPlan {
 #define G_LIMIT 3
 #define G_CONTACT 4
 
+/* ---- the overlaid layouts' narrowphase area (KN) ---- */
+/* convex meshes in the overlaid layouts (ur3e_cvx_wave.h): one wave settles one mesh pair at a time, its
+   GJK simplex and EPA polytope in this LDS work area (wave-uniform state) */
+#define WC_MAXV UR3E_EPA_MAXV
+#define WC_MAXF UR3E_EPA_MAXF
+#define WC_MAXE 64 /* horizon edges of one EPA step held in LDS (convex.h: 3 * UR3E_EPA_MAXF) */
+#define WC_FSLOT ((WC_MAXF + 63) / 64)
+
+/* LDS work area of one mesh pair (wave-uniform state) */
+struct WCvxWork {
+  /* GJK simplex: support points of A - B, A and B, and the closest point's barycentric weights */
+  double sw[4][3], sa[4][3], sb[4][3], slam[4];
+  int sn;
+  /* EPA polytope: vertices (w = a - b, recomputed with convex.h's operation), faces */
+  double pa[WC_MAXV][3], pb[WC_MAXV][3];
+  double fn[WC_MAXF][3], fd[WC_MAXF];
+  int fv[WC_MAXF]; /* i | j << 8 | k << 16, bit 24: alive */
+  int edge[WC_MAXE]; /* horizon edge i | j << 8 */
+  int pnv, pnf, ne;
+  /* plane–convex selection */
+  double psd[UR3E_CVX_PLANE_MAX];
+  int psel[UR3E_CVX_PLANE_MAX];
+};
+
+/* one mesh pair's raw contacts, per survivor slot (filled by the mesh pass before the chunked
+   narrowphase, which emits them at the pair's place in candidate order) */
+template <int MC>
+struct WMeshRes {
+  double raw[MC][7]; /* pos[3], n[3], dist */
+  signed char cnt[W_MAXSURV];
+  unsigned char at[W_MAXSURV];
+  int nraw;
+};
+
+/* the chunked narrowphase's clip polygons of one chunk of survivor lanes ([buf][vertex][coord][lane],
+   conflict-free across lanes) and that chunk's staged raw contacts; the mesh-capable layouts also hold
+   the mesh pass's results (alive through the chunks) and its work area (dead by then, so it shares the
+   chunk buffers' bytes) */
+template <int NPST>
+struct KNChunk {
+  double np_clip[2][8][3][W_NP_LANES];
+  double np_stage[7][NPST]; /* pos[3], n[3], dist */
+  int np_key[NPST];         /* survivor lane * 8 + contact index within the lane */
+  int np_nstage;
+};
+template <int NPST, int MC, bool MESH>
+struct KNArea : KNChunk<NPST> {
+  __device__ __forceinline__ KNChunk<NPST>& chunk() { return *this; }
+};
+template <int NPST, int MC>
+struct KNArea<NPST, MC, true> {
+  union {
+    KNChunk<NPST> ch;
+    WCvxWork cw;
+  };
+  WMeshRes<MC> mres;
+  __device__ __forceinline__ KNChunk<NPST>& chunk() { return ch; }
+};
+
 /* Two LDS layouts.  The full-capacity tier (rows > 64, KSL) keeps every array side by side.  The
    compact tier (rows <= 64: one 64-lane wavefront, register-resident solver) overlays the arrays
    of the position/velocity stages with those of the constraint stages, see the specialisation
@@ -230,13 +289,7 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
             struct { double cacc[K_NB][6]; double cfrc[K_NB][6]; } rne;
           } u;
         };
-        struct { /* KN, collision: clip polygons of one chunk of survivor lanes ([buf][vertex][coord]
-                    [lane], conflict-free across lanes) and that chunk's staged raw contacts */
-          double np_clip[2][8][3][W_NP_LANES];
-          double np_stage[7][NPST]; /* pos[3], n[3], dist */
-          int np_key[NPST];         /* survivor lane * 8 + contact index within the lane */
-          int np_nstage;
-        };
+        KNArea<NPST, MC, MESHES> kn; /* KN, collision (above) */
       };
     };
     struct { /* CR: the stale-kinematics carry, alive only before the first forward (the controller reads it)
@@ -412,6 +465,7 @@ __device__ unsigned long long ur3e_stage_calls[3][W_NSTAGE_MARKS];
 #endif
 
 #include "ur3e_wave_r.h"
+#include "ur3e_cvx_wave.h"
 
 /* ================================================================== */
 /* kinematics (level-parallel over bodies)                             */
@@ -950,26 +1004,36 @@ struct KStageEmit {
 
 /* w_narrow_core with the compact tier's LDS clip buffers and contact stage (lane ln < W_NP_LANES) */
 template <class KS>
-WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
+WD int w_narrow_lds(KModel m, KS& s, int p, int ln, int slot) {
   int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
   double margin = m->cpair_margin[p];
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const KStageEmit<KS::NPST> emit{&s.np_stage[0][0], s.np_key, &s.np_nstage, ln};
+  auto& ch = s.kn.chunk();
+  const KStageEmit<KS::NPST> emit{&ch.np_stage[0][0], ch.np_key, &ch.np_nstage, ln};
   /* convex meshes: the mesh-capable layouts settle a pair whose hulls are apart beyond the margin (GJK,
      or the plane's vertex distances: no contact, the oracle's own decision); a pair that may touch --
      and every mesh pair in the other layouts -- hands the env-step on to the tier that runs EPA */
   if (t2 == UR3E_GEOM_MESH) {
     if constexpr (KS::MESHES) {
-      if (w_mesh_separated(m, s, g1, g2, margin)) return 0;
+      /* settled by the wave in w_mesh_pass: emit its contacts at the pair's place */
+      const int c = s.kn.mres.cnt[slot];
+      const int at = s.kn.mres.at[slot];
+      for (int k = 0; k < c; k++) {
+        const double* r = s.kn.mres.raw[at + k];
+        const double pos[3] = {r[0], r[1], r[2]}, nn[3] = {r[3], r[4], r[5]};
+        emit(k, pos, nn, r[6]);
+      }
+      return c;
+    } else {
+      s.ovf = 1; /* hand the env-step on to the tier that runs the mesh narrowphase */
+      return 0;
     }
-    s.ovf = 1;
-    return 0;
   }
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
     return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2],
                          margin, emit);
   if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX) {
-    KLdsClip clip{&s.np_clip[0][0][0][0], ln};
+    KLdsClip clip{&ch.np_clip[0][0][0][0], ln};
     return k_box_box_t(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
                        m->geom_size[g2], margin, clip, emit);
   }
@@ -979,6 +1043,63 @@ WD int w_narrow_lds(KModel m, KS& s, int p, int ln) {
 template <class KS>
 WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
   return w_pair_near(m, s, p) ? w_narrow_core(m, s, p, raw) : 0;
+}
+
+/* mesh-capable overlaid layouts: every survivor pair with a convex mesh (plane-mesh, box-mesh, mesh-mesh)
+   settled by the whole wave, one pair at a time in candidate order (ur3e_cvx_wave.h: convex.h's results,
+   bit for bit); its raw contacts wait in s.kn.mres until the chunked narrowphase emits them at the pair's
+   place.  More raw contacts than the layout holds, or an EPA horizon beyond WC_MAXE, hand the env-step on. */
+template <class KS>
+WD void w_mesh_pass(KModel m, KS& s, int nsurv) {
+  const int lane = w_lane();
+  auto& R = s.kn.mres;
+  auto& W = s.kn.cw;
+  constexpr int MC = KS::MAXCON;
+  R.cnt[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int slot = lane;
+  const int p = slot < nsurv ? s.cand_off[slot] : 0;
+  const bool mesh = slot < nsurv && m->geom_type[m->cpair_geom2[p]] == UR3E_GEOM_MESH;
+  unsigned long long bm = __ballot(mesh);
+  int nraw = 0;
+  while (bm) {
+    const int q = __builtin_ctzll(bm);
+    bm &= bm - 1;
+    const int pq = rli(p, q);
+    const int g1 = m->cpair_geom1[pq], g2 = m->cpair_geom2[pq];
+    const double margin = m->cpair_margin[pq];
+    WCvxShape B;
+    WCvxLane lb;
+    wc_shape(m, s, g2, B, lb);
+    int c;
+    if (m->geom_type[g1] == UR3E_GEOM_PLANE) {
+      c = wc_plane_convex(s.geom_xpos[g1], s.geom_xmat[g1], B, lb, margin, W, &R.raw[nraw], MC - nraw);
+    } else {
+      WCvxShape A;
+      WCvxLane la;
+      wc_shape(m, s, g1, A, la);
+      double res[7];
+      c = wc_convex_convex(A, la, B, lb, W, margin, res);
+      if (c == 1 && nraw < MC) {
+        if (lane < 7) R.raw[nraw][lane] = lane == 0 ? res[0] : lane == 1 ? res[1] : lane == 2 ? res[2] : lane == 3 ? res[3]
+                                          : lane == 4 ? res[4] : lane == 5 ? res[5] : res[6];
+      }
+    }
+    if (c < 0 || nraw + c > MC) { /* beyond this layout: the next tier settles the env-step */
+      if (lane == 0) s.ovf = 1;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      return;
+    }
+    if (lane == 0) {
+      R.cnt[q] = (signed char)c;
+      R.at[q] = (unsigned char)nraw;
+    }
+    nraw += c;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
 }
 
 /* contact c of the env from raw contact r of candidate pair p */
@@ -1040,7 +1161,9 @@ WD void r_collision(KModel m, KS& s) {
        survivor lane) + (its index), the order of the pass below -- no private (scratch) arrays */
     constexpr int NST = KS::NPST;
     static_assert(KS::BAIL && KS::MAXCON <= NST && NST <= 64, "compact narrowphase stage must hold MAXCON");
-    if (lane == 0) s.np_nstage = 0;
+    if constexpr (KS::MESHES) w_mesh_pass(m, s, nsurv);
+    auto& ch = s.kn.chunk();
+    if (lane == 0) ch.np_nstage = 0;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     const int npl = s.np_lanes;
@@ -1049,7 +1172,7 @@ WD void r_collision(KModel m, KS& s) {
       const bool act = lane < npl && slot < nsurv;
       const int p = s.cand_off[act ? slot : 0];
       int cnt = 0;
-      if (act) cnt = w_narrow_lds(m, s, p, lane);
+      if (act) cnt = w_narrow_lds(m, s, p, lane, slot);
       int incl = cnt;
 #pragma unroll
       for (int d = 1; d < W_NP_LANES; d <<= 1) {
@@ -1060,23 +1183,23 @@ WD void r_collision(KModel m, KS& s) {
       total += rli(incl, W_NP_LANES - 1);
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      const int nall = s.np_nstage;
+      const int nall = ch.np_nstage;
       const int nst = nall < NST ? nall : NST;
-      const int key = lane < nst ? s.np_key[lane] : 0;
+      const int key = lane < nst ? ch.np_key[lane] : 0;
       const int src = key >> 3, kk = key & 7;
       const int offs = shfi(off, src), ps = shfi(p, src);
       if (lane < nst && offs + kk < KS::MAXCON) {
         KRaw r;
-        r.pos[0] = s.np_stage[0][lane]; r.pos[1] = s.np_stage[1][lane]; r.pos[2] = s.np_stage[2][lane];
-        r.n[0] = s.np_stage[3][lane]; r.n[1] = s.np_stage[4][lane]; r.n[2] = s.np_stage[5][lane];
-        r.dist = s.np_stage[6][lane];
+        r.pos[0] = ch.np_stage[0][lane]; r.pos[1] = ch.np_stage[1][lane]; r.pos[2] = ch.np_stage[2][lane];
+        r.n[0] = ch.np_stage[3][lane]; r.n[1] = ch.np_stage[4][lane]; r.n[2] = ch.np_stage[5][lane];
+        r.dist = ch.np_stage[6][lane];
         w_store_contact(m, s, offs + kk, ps, r);
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       if (lane == 0) {
         if (nall > NST) s.ovf = 1; /* contacts were dropped from the stage: > MAXCON anyway */
-        s.np_nstage = 0;
+        ch.np_nstage = 0;
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
