@@ -209,6 +209,11 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
     # (3) every core of the affinity mask (the machine's cores the process may run on)
     host = _host_info()
     n_all = min(host["affinity_cpus"], 512)  # threads count against the box's task limit
+    quota = host.get("cgroup_cpu_quota")
+    if isinstance(quota, float) and quota < n_all:
+        # the cgroup's CPU bandwidth limit, not the affinity mask, is what the threads can use: more threads
+        # than the quota only time-share it (round 4 measured 256 threads 28x slower than 16)
+        n_all = max(int(quota), 1)
     all_cores = None
     if n_all != threads:
         L.ur3o_set_threads(n_all)
@@ -216,12 +221,10 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         rng = np.random.default_rng(seed + 2)
         dta = _time_oracle(oba, lambda _: rng.uniform(lo, hi, size=(n_envs_sample, 4)), all_cores_steps)
         del oba
-        quota = host.get("cgroup_cpu_quota")
-        capped = (f"; the cgroup's CPU quota is {quota} CPUs, so the {n_all} threads time-share that many"
-                  if isinstance(quota, float) and quota < n_all else "")
         all_cores = {"value": n_envs_sample * all_cores_steps / dta, "unit": "env-steps/s", "cores": n_all,
                      "sample": f"{n_envs_sample} envs x {all_cores_steps} env-steps from reset, OpenMP {n_all} "
-                               f"threads (every CPU of the affinity mask), {dta:.1f} s{capped}"}
+                               f"threads (the affinity mask's CPUs, capped at the cgroup's CPU quota {quota}), "
+                               f"{dta:.1f} s"}
     L.ur3o_set_threads(threads)
     try:
         others = cpu_other_configs(L, threads)
@@ -298,7 +301,7 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
     tc = [x - y for x, y in zip(bm.tier_counts(), tc0)]
     tot = float(n_envs * (warmup + steps))
     out["main_mesh_gym_v2"] = {"value": val, "unit": "env-steps/s", "envs": n_envs, "substeps_per_env_step": 2,
-                               "model": "main.xml with convex meshes (24 colliding geoms, 17 meshes, 234 pairs)",
+                               "model": MODEL_VARIANT["main_mesh"],
                                "kernel_resources": bm.kernel_info(),
                                "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
                                "grasp_tier_routed_frac": tc[2] / tot}
@@ -353,7 +356,87 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
         "records": "traj_true [rows, N, 7] and actuator_frc [rows, N, 7] every row, on the device",
         "grasp_rows_recorded_frac": float(tt[:, :, 6].mean().item())}
     drv.close()
+    # C3 on main.xml with its convex meshes (the reference's collision set): the whole grasp and carry, tier
+    # fractions included (the closed gripper's linkage meshes touch every carry row: EPA in the wavefront)
+    out["C3_main_mesh_move_l_mug"] = c3_mesh(n_envs)
+    try:
+        out["C5_ppo_rollout"] = c5_ppo_rollout(n_envs)
+    except Exception as e:  # secondary numbers never fail the headline line
+        out["C5_ppo_rollout"] = {"error": repr(e)}
     return out
+
+
+def c3_mesh(n_envs=4096, rows=(1500, 5000)):
+    """C3 (move_l_mug scripted pick) on main.xml compiled with convex stand-in hulls for its mesh files: rows
+    rows[0]..rows[1] (descent, grasp, lift and carry; the approach untimed), HIP events on the library
+    stream, with the tier fractions (full_tier_frac: env-steps that needed the full-capacity tier)"""
+    import torch
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    drv = MoveLMug(n_envs, reset_mode="low", seed=0, model="main_mesh")
+    g0, g1 = rows
+    for t in range(g0):
+        drv.batch.step(drv.traj.row(t))
+    rows_t = [drv.traj.row(t) for t in range(g0, g1)]
+    tc0 = drv.batch.tier_counts()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for r in rows_t:
+        drv.batch.step(r)
+    e1.record()
+    torch.cuda.synchronize()
+    tc = [x - y for x, y in zip(drv.batch.tier_counts(), tc0)]
+    tot = float(n_envs * (g1 - g0))
+    res = {"value": tot / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s", "envs": n_envs,
+           "substeps_per_env_step": 1, "rows": [g0, g1], "model": MODEL_VARIANT["main_mesh"],
+           "kernel_resources": drv.batch.kernel_info(),
+           "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot}
+    drv.close()
+    return res
+
+
+
+def c5_ppo_rollout(n_envs=4096, n_steps=16, iterations=3):
+    """BASELINE config C5 on one GPU: SB3 PPO as gymnasium_src/scripts/regular_rl/rl/train_rl.py:38-90 runs it
+    (config_rl.yml: n_steps 16, batch 256, 30 epochs, net_arch [256, 256]; VecNormalize(norm_obs, clip 10),
+    train_rl.py:57), restated on the device (ur3e_amd/rl/ppo.py: SB3 is not installed): the UR3eVecEnv
+    (this library) -> on-device VecNormalize -> the actor-critic's forward, no host round trip.  Reported:
+    the rollout's env-steps/s (env + normalisation + policy), the same env-steps through the env and
+    VecNormalize alone with resident actions (the env's share), and the PPO update per iteration."""
+    import torch
+    from ur3e_amd.envs.vec_env import UR3eVecEnv
+    from ur3e_amd.envs.vec_normalize import VecNormalize
+    from ur3e_amd.rl.ppo import PPO
+    venv = UR3eVecEnv(num_envs=n_envs, device=0, seed=0)
+    env = VecNormalize(venv, norm_obs=True, norm_reward=False, clip_obs=10.0)
+    algo = PPO(env, n_steps=n_steps, batch_size=256, n_epochs=30, device="cuda:0", seed=0)
+    algo.learn(1)  # warm-up: allocations, graph capture, first kernels
+    times = algo.learn(iterations)
+    roll = sum(t["rollout_s"] for t in times) / iterations
+    train = sum(t["train_s"] for t in times) / iterations
+    lo = torch.as_tensor(env.action_space.low, dtype=torch.float64, device="cuda")
+    hi = torch.as_tensor(env.action_space.high, dtype=torch.float64, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    acts = lo + (hi - lo) * torch.rand((n_steps * iterations, n_envs, lo.numel()), dtype=torch.float64, device="cuda",
+                                       generator=g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a in acts:
+        env.step_torch(a)
+    torch.cuda.synchronize()
+    env_s = (time.perf_counter() - t0) / iterations
+    venv.close()
+    k = n_steps * n_envs
+    return {"value": k / roll, "unit": "env-steps/s", "envs": n_envs,
+            "what": "PPO rollout: env + on-device VecNormalize + policy inference ([256, 256] tanh MLP, f32)",
+            "env_and_vecnormalize_only": {"value": k / env_s, "unit": "env-steps/s"},
+            "policy_share_of_rollout": 1.0 - env_s / roll,
+            "rollout_ms_per_env_step": 1e3 * roll / n_steps,
+            "ppo_update_s_per_iteration": train,
+            "iteration_env_steps_per_s": k / (roll + train),
+            "config": {"n_steps": n_steps, "batch_size": 256, "n_epochs": 30, "iterations_timed": iterations,
+                       "source": "ur3e_amd/rl/ppo.py (SB3 PPO restated; SB3 absent)"}}
 
 
 def move_l_mug_parity(n_envs=512, steps=1000, seed=0):

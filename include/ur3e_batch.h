@@ -232,10 +232,21 @@ int ur3e_batch_set_queue_split(ur3e_batch_t* b, int percent);
    in rank order into d_*_all ([nranks * n] rows; other ranks pass NULL).  Every rank's handle has the
    same n; the shards are contiguous global env ids (env_id_offset = rank * n).  Enqueued on `stream` as
    one point-to-point group, after the step that filled the buffers.  The env path itself has no
-   collective. */
+   collective.  PRECONDITION: every rank's handle has the same n and obs_dim (the same env id); the root
+   posts receives of exactly its own sizes, so ranks that disagree leave the group's transfers unmatched
+   (RCCL then hangs the streams) -- nothing here can detect it without a collective of its own.
+   Replaces the reference's SubprocVecEnv gather of per-env step results (train_rl.py:38-44,
+   stable_baselines3 make_vec_env), as north_star config C4 prescribes. */
 int ur3e_batch_gather(ur3e_batch_t* b, void* rccl_comm, int root, const double* d_obs, const double* d_reward,
                       const uint8_t* d_terminated, const uint8_t* d_truncated, double* d_obs_all,
                       double* d_reward_all, uint8_t* d_terminated_all, uint8_t* d_truncated_all, void* stream);
+
+/* ur3e_batch_gather with explicit sizes, for host-managed buffers (the handle only supplies n and
+   obs_dim): the same point-to-point group, rank p's rows at [p * n, (p + 1) * n) of the root's buffers;
+   the same precondition (equal n and obs_dim on every rank). */
+int ur3e_gather_rows(void* rccl_comm, int root, int n, int obs_dim, const double* d_obs, const double* d_reward,
+                     const uint8_t* d_terminated, const uint8_t* d_truncated, double* d_obs_all, double* d_reward_all,
+                     uint8_t* d_terminated_all, uint8_t* d_truncated_all, void* stream);
 
 /* diagnostic (the queue's forward-progress test): launch `workgroups` workgroups on `stream` that each
    hold 64 KB of LDS (two per CU leave room for one step workgroup) for hold_us microseconds, and

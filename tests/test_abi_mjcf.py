@@ -91,6 +91,31 @@ def test_missing_mjcf_is_an_error(driver, tmp_path):
     assert r.returncode == 1 and "ur3e_model_from_mjcf" in r.stderr
 
 
+def test_missing_libpython_is_an_error_code(driver, tmp_path):
+    """UR3E_LIBPYTHON naming a library that does not exist (a C host without an interpreter linked in): the
+    entry point returns UR3E_EINVAL with the loader's message -- no crash out of the extern "C" call."""
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env["UR3E_LIBPYTHON"] = str(tmp_path / "no_such_libpython.so")
+    r = subprocess.run([driver, "image", os.path.join(ASSETS, "kat_box_plane.xml"), str(tmp_path / "m.bin")],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 1, (r.returncode, r.stderr)
+    assert "libpython not found" in r.stderr and "no_such_libpython.so" in r.stderr
+
+
+def test_non_ascii_paths(driver, tmp_path):
+    """An MJCF (and its mesh files) under a directory whose name is not ASCII, and an output path there: the
+    embedded compiler receives the same bytes (a bytes literal decoded with the filesystem encoding)."""
+    import shutil
+    from ur3e_amd.model.compiler import compile_mjcf, to_ctypes
+    d = tmp_path / "modèle_ä"
+    shutil.copytree(ASSETS, d)
+    out = d / "sortie_é.bin"
+    r = _run([driver, "image", str(d / "mesh_scene.xml"), str(out)], cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == bytes(to_ctypes(compile_mjcf(os.path.join(ASSETS, "mesh_scene.xml"))))
+
+
 def test_in_process_ctypes_uses_the_running_interpreter():
     from ur3e_amd import runtime as rt
     from ur3e_amd.model.compiler import compile_mjcf, to_ctypes

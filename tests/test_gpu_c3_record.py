@@ -37,8 +37,10 @@ def test_move_l_mug_records_every_row_bit_exact():
         np.testing.assert_array_equal(tt[t], ob.task_space_state(tl, tr), err_msg=f"traj_true row {t}")
         np.testing.assert_array_equal(af[t], ob.actuator_force(), err_msg=f"actuator_frc row {t}")
         grip += int(tt[t, :, 6].sum())
-    # the flag is the lexicographic touch test; with the box-surrogate pads the pad contacts of this
-    # pick mostly fall outside the narrow pad1 sites, so the flag may stay 0 -- it is compared above
+    # the flag is the lexicographic touch test; in this pick every pad1-mug contact sits on a corner of the
+    # reference's own pad box (|x| = 0.011 at its top edge), outside the pad1 touch site (|x| <= 0.01,
+    # main.xml:192), so both touch readings and the flag stay 0 (pinned on the oracle's contact positions in
+    # tests/test_c3_grasp_flag_cpu.py) -- it is compared above
     assert np.isin(tt[:, :, 6], (0.0, 1.0)).all()
     print(f"rows x envs with the grasp flag set: {grip}")
     assert np.abs(af[:, :, 6]).max() > 0 and np.ptp(tt[:, :, 0:6], axis=0).max() > 0.01
@@ -102,3 +104,33 @@ def test_grasp_flag_set_from_pad_contact_states():
     assert np.isin(f, (0.0, 1.0)).all()
     assert (f == 1.0).sum() >= n and (f == 0.0).sum() > 0, f.sum(axis=0)
     gb.close()
+
+
+def test_scripted_pick_wide_tier_cap_bit_exact():
+    """The scripted pick runs the wider compact tier (KSS_NV_W: 10 contacts / 44 rows).  A positive diagnostic
+    contact cap applies to it too (advisor finding, round 4): with cap 3, env-steps of more than 3 contacts
+    (the descent onto the mug and the grasp) overflow mid-step and the grasp tier recomputes them; every
+    row stays bit-exact against the oracle and none reaches the full-capacity tier."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    n, rows = 32, 2200
+    drv = MoveLMug(n, reset_mode="low", seed=2, tier_con_cap=3)
+    gb = drv.batch
+    ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n)
+    for t in range(rows):
+        row = drv.step()
+        ob.step(row.cpu().numpy())
+        if t % 100 == 99:
+            torch.cuda.synchronize()
+            qp, qv, wa = gb.get_state()
+            oqp, oqv, owa, onc = ob.get_state()
+            np.testing.assert_array_equal(qp.cpu().numpy(), oqp, err_msg=f"qpos row {t}")
+            np.testing.assert_array_equal(qv.cpu().numpy(), oqv, err_msg=f"qvel row {t}")
+            np.testing.assert_array_equal(gb.get_info()["ncon"].cpu().numpy(), onc, err_msg=f"ncon row {t}")
+    tc = gb.tier_counts()
+    print("tier counts (compact bails, full tier, routed):", tc)
+    assert tc[0] > 0 and tc[1] == 0
+    drv.close()

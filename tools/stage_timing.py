@@ -2,6 +2,7 @@
 Never quote this build's run time (its atomics serialise lane 0); read the SHARES.
 
 usage: stage_timing.py [n_envs] [envs_per_block] [workload: gym | c3] [tier: 0 compact | 1 grasp | 2 full]
+       (UR3E_STAGE_MODEL=main_mesh: main.xml with its convex meshes)
   gym: gym ur3e-v2 random actions (2 substeps, per-env-step launch so the stage marks run);
   c3:  the scripted move_l_mug pick (1 substep per row) timed over its grasp rows 1850..2100, where
        routed envs run in the grasp tier."""
@@ -30,16 +31,18 @@ names = {24: "load state+action+carry", 35: "controller (lane 0, substep 0)", 23
          36: "(r) constraint rows: layout", 37: "(r) constraint rows: group data", 38: "(r) constraint rows: Jacobian",
          39: "(r) collision: broadphase", 40: "(r) tree LDL' factor (smooth + Euler)",
          41: "(r) eval: J.qacc, M.qacc", 42: "(r) eval: constraint update", 43: "(r) eval: cost sums",
-         44: "(r) grad: J'f", 45: "(r) ls eval: row terms", 46: "(r) ls eval: sums", 47: "(r) direction: cone Hessians"}
+         44: "(r) grad: J'f", 45: "(r) ls eval: row terms", 46: "(r) ls eval: sums", 47: "(r) direction: cone Hessians",
+         48: "(r) collision: mesh pairs (wave GJK/EPA)"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"
 tier = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 L = rt.load_library()
 L.ur3e_debug_stage_cycles_tier.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-cyc = (ctypes.c_ulonglong * 48)(); calls = (ctypes.c_ulonglong * 48)()
+cyc = (ctypes.c_ulonglong * 50)(); calls = (ctypes.c_ulonglong * 50)()
+MODEL = os.environ.get("UR3E_STAGE_MODEL", "main")  # main | main_mesh
 if work == "gym":
-    md, mc = rt.load_model("main")
+    md, mc = rt.load_model(MODEL)
     # schedule 1: the per-env-step kernel (the one with stage marks)
     b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=1, envs_per_block=epb,
                                     schedule=1), n)
@@ -51,7 +54,7 @@ if work == "gym":
     steps = [lambda: b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))] * K
 else:
     from ur3e_amd.controller.move_l_mug import MoveLMug
-    drv = MoveLMug(n, reset_mode="low", seed=0)
+    drv = MoveLMug(n, reset_mode="low", seed=0, model=MODEL)
     b = drv.batch
     r0, K, subs = 1850, 250, 1
     for t in range(r0):

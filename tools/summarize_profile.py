@@ -2,11 +2,15 @@
 
 HBM bytes per launch follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE are
 collected in separate passes, both in KiB; on gfx950 FETCH_SIZE counts one half of each wide
-coalesced read, so the fetch figure is doubled.  usage: summarize_profile.py gpurun_out/<run> <name> [round]"""
+coalesced read, so the fetch figure is doubled.
+usage: summarize_profile.py gpurun_out/<run> <name> [round] [kind: traffic | traffic_mesh]
+(bench.py reads profiles/<kind>_<round>.json: `traffic` for the headline model, `traffic_mesh` for
+--model main_mesh)"""
 import csv, json, os, shutil, sys
 
 src, name = sys.argv[1], sys.argv[2]
-rnd = sys.argv[3] if len(sys.argv) > 3 else "r04"
+rnd = sys.argv[3] if len(sys.argv) > 3 else "r05"
+kind = sys.argv[4] if len(sys.argv) > 4 else "traffic"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(REPO, "profiles", name)
 os.makedirs(dst, exist_ok=True)
@@ -44,7 +48,11 @@ hbm = dict(kernel=kname.split("(")[0], envs_per_launch=4096,
            hbm_bytes_per_launch=(2 * fkb + wkb) * 1024,
            launch_resources=dict(lds_bytes=fe[0]["lds"], scratch_bytes_per_lane=fe[0]["scratch"],
                                  vgpr=fe[0]["vgpr"], agpr=fe[0]["agpr"]),
-           note="FETCH_SIZE doubled (gfx950 wide-read correction); KiB units from rocprofv3")
+           note="FETCH_SIZE doubled (gfx950 wide-read correction); KiB units from rocprofv3. launch_resources are "
+                "rocprofv3's dispatch fields: lds_bytes is the STATIC group segment rounded to its 512 B granule "
+                "(the working set is dynamic LDS, w_dyn_lds, which the dispatch record leaves out) and vgpr is "
+                "the descriptor's VGPR granule count x 4 (gfx950 wave64 allocates VGPRs in granules of 8), so "
+                "the code object's figures (tools/kinfo.py, bench kernel_resources) are the ones to quote")
 json.dump(hbm, open(os.path.join(dst, "pmc_hbm.json"), "w"), indent=1)
 sq = counters(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
 sqs = {k: per_launch(v) for k, v in sq.items()}
@@ -68,7 +76,7 @@ dirty = subprocess.run(["git", "-C", REPO, "status", "--porcelain", "--untracked
                         "include"], capture_output=True, text=True).stdout.strip()
 json.dump({"hbm_bytes_per_launch": hbm["hbm_bytes_per_launch"], "source": f"profiles/{name}/pmc_hbm.json",
            "head": head + ("+dirty-csrc" if dirty else ""), "kernel": hbm["kernel"]},
-          open(os.path.join(REPO, "profiles", f"traffic_{rnd}.json"), "w"))
+          open(os.path.join(REPO, "profiles", f"{kind}_{rnd}.json"), "w"))
 stats = list(csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))))
 for r in stats[:4]:
     print(r["Name"][:70], r["Calls"], float(r["AverageNs"]) / 1e6, "ms")

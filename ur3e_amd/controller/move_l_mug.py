@@ -42,7 +42,7 @@ class MoveLMug:
 
     def __init__(self, n_envs: int, reset_mode: str = "deterministic", device: int = 0, seed: int = 0,
                  envs_per_block: int = 0, sensors: bool = False, config_yaml_path: str | None = None,
-                 model: str = "main"):
+                 model: str = "main", tier_con_cap: int = 0):
         """sensors=True also keeps the full mjData.sensordata (incl. the torque sensors) readable through
         batch.get_sensordata() after a step, at the cost of the full-capacity kernel (see
         ur3e_config_t.sensors).  The reference's per-row records -- traj_true (get_task_space_state) and
@@ -58,7 +58,7 @@ class MoveLMug:
         # controller/move_l_mug.py:20-26: gains from config_l_mug.yml
         cfg = rt.make_config(task=rt.TASK_TRAJ_L, frame_skip=1, max_episode_steps=0, auto_reset=False,
                              reset_noise=NOISE[reset_mode], reset_key=md["id_key_down"], model=md, seed=seed,
-                             envs_per_block=envs_per_block, sensors=sensors,
+                             envs_per_block=envs_per_block, sensors=sensors, tier_con_cap=tier_con_cap,
                              task_gains=gains.task_gains(config_yaml_path))
         self.batch = rt.Batch(mc, cfg, n_envs, device=device)   # reset_with_mug (keyframe + forward)
         obs = self.batch.obs

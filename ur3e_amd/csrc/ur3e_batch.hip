@@ -937,7 +937,9 @@ WD void w_load(KModel m, const KConfig& c, const KState& st, int e, KS& s, WOut&
        the step then always launches behind it), < 0 caps every bailing tier (compact and grasp: the envs
        reach the full-capacity tier) */
     const int cap = c.tier_con_cap, capv = cap > 0 ? cap : -cap;
-    const bool capped = KS::BAIL && (cap < 0 || (cap > 0 && KS::MAXCON <= W_SMALL_MAXCON));
+    /* the compact tiers: the gym layout and the scripted pick's wider one (KSS_NV_W / KSS_NV_MW) */
+    constexpr bool compact = KS::OVERLAY && KS::MAXCON <= W_WIDE_MAXCON;
+    const bool capped = KS::BAIL && (cap < 0 || (cap > 0 && compact));
     s.cap_con = (capped && capv < KS::MAXCON) ? capv : KS::MAXCON;
     if constexpr (KS::OVERLAY) s.np_lanes = c.np_lanes;
     else s.sens = c.sensors;
@@ -2005,7 +2007,8 @@ struct ur3e_batch {
   int* d_qctl;     /* {next unit per queue [W_NQUEUE], workgroups done, epoch} */
   int* d_flags;    /* [n] per-env substep hand-off flags */
   double* d_mid;   /* [n][W_MID] mid-step state */
-  double* d_half;  /* [n][w_half_words] the split units' working-set hand-off (queue) */
+  double* d_half;  /* [n][w_half_words] the split units' working-set hand-off (queue; null while no split) */
+  size_t half_bytes;
   ur3e_model_t host_model;
   ur3e_model_t* d_model;
   KPlan* d_plan;
@@ -2205,8 +2208,8 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     const double rv[3] = {-1.209, -1.209, 1.209};
     k_quat_from_rotvec(rv, c.gym_qd);
   }
-  /* the scripted pick (TRAJ_L) on main.xml runs the wider compact tier (KSS_NV_W) */
-  b->wide = tiered && main_tree && !mesh && cfg->task == UR3E_TASK_TRAJ_L;
+  /* the scripted pick (TRAJ_L) on main.xml runs the wider compact tier (KSS_NV_W; with meshes KSS_NV_MW) */
+  b->wide = tiered && main_tree && cfg->task == UR3E_TASK_TRAJ_L;
   c.route_ncon = b->wide ? W_WIDE_MAXCON - 2 : W_SMALL_MAXCON - 1;
   c.route_nefc = b->wide ? W_WIDE_MAXEFC - 8 : W_SMALL_MAXEFC - 3;
   for (int k = 0; k < 12; k++) {
@@ -2293,7 +2296,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
      (cfg->schedule 1 keeps one workgroup per env-step) */
   b->queued = tiered && b->main_tree && k_is_gym(cfg->task) && c.frame_skip > 1 &&
               c.frame_skip < W_FLAG_CLAIMED && cfg->schedule != 1; /* flag codes: substeps done < 14 */
-  b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->d_half = nullptr; b->q_grid = 0;
+  b->d_qctl = nullptr; b->d_flags = nullptr; b->d_mid = nullptr; b->d_half = nullptr; b->half_bytes = 0; b->q_grid = 0;
   if (b->queued) {
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -2324,8 +2327,10 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMalloc(&b->d_flags, sizeof(int) * nd));
     HIPCHK(hipMemset(b->d_flags, 0, sizeof(int) * nd));
     HIPCHK(hipMalloc(&b->d_mid, sizeof(double) * nd * W_MID));
-    const size_t hw = (size_t)(b->mesh ? w_half_words<KSS_NV_M>() : w_half_words<KSS_NV>());
-    HIPCHK(hipMalloc(&b->d_half, 16 * hw * nd));
+    /* the split units' hand-off records (16.5 KB per env) only when a split is on: allocated here for a
+       nonzero build default, else by ur3e_batch_set_queue_split (null disables the split in the kernel) */
+    b->half_bytes = 16 * (size_t)(b->mesh ? w_half_words<KSS_NV_M>() : w_half_words<KSS_NV>()) * nd;
+    if (W_SPLIT_PERCENT > 0) HIPCHK(hipMalloc(&b->d_half, b->half_bytes));
     /* the last W_SPLIT_PERCENT % of each queue's envs run their last substep as two half units (0: none) */
     const int nper = n_envs / nq;
     b->cfg.split_from = nper - nper * W_SPLIT_PERCENT / 100;
@@ -2434,6 +2439,10 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
                          b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
                          d_terminal_obs, c_list, c_ctl, b->d_qctl, b->d_flags, b->d_mid,
                          b->d_ovf_total + 3, b->d_half);
+    else if (b->wide)
+      hipLaunchKernelGGL((w_env_step<64, KSW, UR3E_TASK_TRAJ_L>), dim3(b->n), dim3(64), w_dyn_lds<KSW>(), st, b->d_model,
+                         b->d_plan, b->cfg, kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated,
+                         d_terminal_obs, c_list, c_ctl);
     else
       hipLaunchKernelGGL((w_env_step<64, KSC>), dim3(b->n), dim3(64), w_dyn_lds<KSC>(), st, b->d_model, b->d_plan, b->cfg,
                          kst, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
@@ -2528,7 +2537,7 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
       pre = capturing || (b->last_route >= 0 && b->hstep - b->last_route < W_ROUTE_HOLD);
       if (!pre) kst.route = nullptr;
     }
-    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M, KSS_NV_M>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M, KSS_NV_MW>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                       d_terminated, d_truncated, d_terminal_obs)
                            : launch_tiers<KSS_NV, KSG_NV, KSL, KSS_NV_W>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                 d_terminated, d_truncated, d_terminal_obs);
@@ -2721,8 +2730,9 @@ extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* ld
   if (b->tiered) {
     nt = 64;
     if (b->mesh) {
-      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2> : (const void*)w_env_step<64, KSS_NV_M>;
-      dyn = w_dyn_lds<KSS_NV_M>();
+      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2>
+           : b->wide ? (const void*)w_env_step<64, KSS_NV_MW, UR3E_TASK_TRAJ_L> : (const void*)w_env_step<64, KSS_NV_M>;
+      dyn = b->wide ? w_dyn_lds<KSS_NV_MW>() : w_dyn_lds<KSS_NV_M>();
     } else {
       fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
            : b->wide ? (const void*)w_env_step<64, KSS_NV_W, UR3E_TASK_TRAJ_L>
@@ -2825,6 +2835,10 @@ extern "C" int ur3e_batch_set_queue_split(ur3e_batch_t* b, int percent) {
   if (!b) return fail(UR3E_EINVAL, "null handle");
   if (percent < 0 || percent > 100) return fail(UR3E_EINVAL, "split percent outside [0, 100]");
   if (!b->queued) return percent ? fail(UR3E_EINVAL, "the handle does not run the substep work queue") : UR3E_OK;
+  if (percent > 0 && !b->d_half) {
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMalloc(&b->d_half, b->half_bytes));
+  }
   const int nper = b->n / ((b->n & 7) ? 1 : W_NQUEUE);
   b->cfg.split_from = nper - nper * percent / 100;
   return UR3E_OK;

@@ -11,6 +11,7 @@
  * (ncclComm_t passed as void*).
  */
 #include <dlfcn.h>
+#include <stdlib.h>
 
 #include <string>
 
@@ -42,8 +43,15 @@ bool load_rccl(Rccl& r, std::string& err) {
     return true;
   }
   void* h = nullptr;
-  for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-    if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+  /* UR3E_RCCL_LIB: another library with RCCL's point-to-point API (the CPU test's in-process fake,
+     tests/c/fake_rccl.c, drives the rank-offset arithmetic below with several ranks and no GPU) */
+  const char* over = getenv("UR3E_RCCL_LIB");
+  if (over && *over) {
+    h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+  } else {
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+  }
   if (!h) {
     err = "librccl not found";
     return false;
@@ -68,12 +76,13 @@ bool load_rccl(Rccl& r, std::string& err) {
 
 }  // namespace
 
-extern "C" int ur3e_batch_gather(ur3e_batch_t* b, void* rccl_comm, int root, const double* d_obs,
-                                 const double* d_reward, const uint8_t* d_terminated, const uint8_t* d_truncated,
-                                 double* d_obs_all, double* d_reward_all, uint8_t* d_terminated_all,
-                                 uint8_t* d_truncated_all, void* stream) {
-  if (!b || !rccl_comm || !d_obs || !d_reward || !d_terminated || !d_truncated)
-    return fail(UR3E_EINVAL, "null handle, communicator or buffer");
+extern "C" int ur3e_gather_rows(void* rccl_comm, int root, int n, int obs_dim, const double* d_obs,
+                                const double* d_reward, const uint8_t* d_terminated, const uint8_t* d_truncated,
+                                double* d_obs_all, double* d_reward_all, uint8_t* d_terminated_all,
+                                uint8_t* d_truncated_all, void* stream) {
+  if (!rccl_comm || !d_obs || !d_reward || !d_terminated || !d_truncated)
+    return fail(UR3E_EINVAL, "null communicator or buffer");
+  if (n <= 0 || obs_dim <= 0) return fail(UR3E_EINVAL, "n and obs_dim must be positive");
   Rccl r;
   std::string err;
   if (!load_rccl(r, err)) return fail(UR3E_EINVAL, err);
@@ -83,20 +92,32 @@ extern "C" int ur3e_batch_gather(ur3e_batch_t* b, void* rccl_comm, int root, con
   if (root < 0 || root >= nranks) return fail(UR3E_EINVAL, "root outside the communicator");
   if (rank == root && (!d_obs_all || !d_reward_all || !d_terminated_all || !d_truncated_all))
     return fail(UR3E_EINVAL, "the root needs the gathered buffers");
-  const size_t n = (size_t)ur3e_batch_num_envs(b), od = (size_t)ur3e_batch_obs_dim(b);
+  /* rank p's rows land at rows [p * n, (p + 1) * n) of the root's buffers: every rank must pass the same
+     n and obs_dim (a precondition, include/ur3e_batch.h), or the send and receive counts disagree */
+  const size_t nn = (size_t)n, od = (size_t)obs_dim;
   int rc = r.GroupStart();
-  if (!rc) rc = r.Send(d_obs, n * od, kFloat64, root, rccl_comm, stream);
-  if (!rc) rc = r.Send(d_reward, n, kFloat64, root, rccl_comm, stream);
-  if (!rc) rc = r.Send(d_terminated, n, kUint8, root, rccl_comm, stream);
-  if (!rc) rc = r.Send(d_truncated, n, kUint8, root, rccl_comm, stream);
+  if (!rc) rc = r.Send(d_obs, nn * od, kFloat64, root, rccl_comm, stream);
+  if (!rc) rc = r.Send(d_reward, nn, kFloat64, root, rccl_comm, stream);
+  if (!rc) rc = r.Send(d_terminated, nn, kUint8, root, rccl_comm, stream);
+  if (!rc) rc = r.Send(d_truncated, nn, kUint8, root, rccl_comm, stream);
   if (rank == root)
     for (int p = 0; p < nranks && !rc; p++) {
-      rc = r.Recv(d_obs_all + (size_t)p * n * od, n * od, kFloat64, p, rccl_comm, stream);
-      if (!rc) rc = r.Recv(d_reward_all + (size_t)p * n, n, kFloat64, p, rccl_comm, stream);
-      if (!rc) rc = r.Recv(d_terminated_all + (size_t)p * n, n, kUint8, p, rccl_comm, stream);
-      if (!rc) rc = r.Recv(d_truncated_all + (size_t)p * n, n, kUint8, p, rccl_comm, stream);
+      rc = r.Recv(d_obs_all + (size_t)p * nn * od, nn * od, kFloat64, p, rccl_comm, stream);
+      if (!rc) rc = r.Recv(d_reward_all + (size_t)p * nn, nn, kFloat64, p, rccl_comm, stream);
+      if (!rc) rc = r.Recv(d_terminated_all + (size_t)p * nn, nn, kUint8, p, rccl_comm, stream);
+      if (!rc) rc = r.Recv(d_truncated_all + (size_t)p * nn, nn, kUint8, p, rccl_comm, stream);
     }
   const int rc2 = r.GroupEnd();
   if (rc || rc2) return fail(UR3E_EHIP, std::string("RCCL: ") + r.GetErrorString(rc ? rc : rc2));
   return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_gather(ur3e_batch_t* b, void* rccl_comm, int root, const double* d_obs,
+                                 const double* d_reward, const uint8_t* d_terminated, const uint8_t* d_truncated,
+                                 double* d_obs_all, double* d_reward_all, uint8_t* d_terminated_all,
+                                 uint8_t* d_truncated_all, void* stream) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  return ur3e_gather_rows(rccl_comm, root, ur3e_batch_num_envs(b), ur3e_batch_obs_dim(b), d_obs, d_reward,
+                          d_terminated, d_truncated, d_obs_all, d_reward_all, d_terminated_all, d_truncated_all,
+                          stream);
 }

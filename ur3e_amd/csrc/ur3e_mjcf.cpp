@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/ur3e_batch.h"
+#include "gen_pyconfig.h"
 
 __attribute__((visibility("hidden"))) int ur3e_internal_fail(int code, const char* msg);
 
@@ -57,17 +58,29 @@ bool load_python(PyApi& p, std::string& err) {
      exports them); loading libpython beside it would start a second interpreter */
   void* h = RTLD_DEFAULT; /* (a null handle on glibc: `found` says whether it serves) */
   bool found = dlsym(RTLD_DEFAULT, "Py_IsInitialized") != nullptr;
+  /* UR3E_LIBPYTHON, when set, is the only candidate; otherwise the libpython of the interpreter that built
+     this library (gen_pyconfig.h, written by ur3e_amd/_build.py), then the same version's soname, then
+     the stable-ABI soname */
   std::vector<std::string> names;
-  if (const char* e = getenv("UR3E_LIBPYTHON")) names.push_back(e);
-  names.push_back("libpython3.10.so.1.0");
-  names.push_back("libpython3.10.so");
-  names.push_back("libpython3.so");
+  if (const char* e = getenv("UR3E_LIBPYTHON")) {
+    names.push_back(e);
+  } else {
+    names.push_back(UR3E_BUILD_LIBPYTHON);
+    names.push_back(UR3E_BUILD_LIBPYTHON_SONAME);
+    names.push_back("libpython3.so");
+  }
+  std::string last;
   for (size_t k = 0; !found && k < names.size(); k++) {
+    if (names[k].empty()) continue;
     h = dlopen(names[k].c_str(), RTLD_NOW | RTLD_GLOBAL);
     found = h != nullptr;
+    if (!found) {
+      const char* de = dlerror(); /* read once: the call clears it */
+      last = de ? de : "";
+    }
   }
   if (!found) {
-    err = "libpython not found (set UR3E_LIBPYTHON): " + std::string(dlerror() ? dlerror() : "");
+    err = "libpython not found (set UR3E_LIBPYTHON): " + last;
     return false;
   }
   PyApi q;
@@ -88,9 +101,11 @@ bool load_python(PyApi& p, std::string& err) {
   return true;
 }
 
-/* a Python string literal for s */
+/* a Python str expression for s: a bytes literal (every byte >= 128 or < 32 escaped) decoded with the
+   filesystem encoding, so that a path's non-ASCII bytes arrive as the same path (a str literal would read
+   each escaped byte as a code point) */
 std::string pyquote(const std::string& s) {
-  std::string o = "'";
+  std::string o = "__import__('os').fsdecode(b'";
   for (unsigned char ch : s) {
     if (ch == '\\' || ch == '\'') {
       o += '\\';
@@ -103,7 +118,7 @@ std::string pyquote(const std::string& s) {
       o += (char)ch;
     }
   }
-  return o + "'";
+  return o + "')";
 }
 
 /* the directory holding the ur3e_amd package: two levels above this library (ur3e_amd/_lib/x.so) */

@@ -41,7 +41,7 @@
 
 /* host-precomputed tree bookkeeping for the cooperative stages */
 /* stage-timing marks of the -DUR3E_STAGE_TIMING build (tools/stage_timing.py) */
-#define W_NSTAGE_MARKS 48
+#define W_NSTAGE_MARKS 50
 
 struct KPlan {
   int nlevel;
@@ -383,6 +383,9 @@ typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true> KSG_NV;
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSS_NV_M;
 typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
 typedef KSX<K_MAXCON, K_MAXEFC, 0, 0, false, K_NG_MESH> KSL_M;
+/* the scripted pick's wider compact tier (10 contacts / 44 rows) with the mesh geoms: its carry rows hold the
+   mug on the table, the pads and the closed fingers' linkage meshes (7-8 contacts) */
+typedef KSX<W_WIDE_MAXCON, W_WIDE_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSS_NV_MW;
 #define NVOF(KS, m) ((KS::NV) ? (KS::NV) : (m)->nv)
 
 /* Barrier between cooperative phases.  With one 64-lane wavefront per env (NT == 64) the
@@ -1161,7 +1164,10 @@ WD void r_collision(KModel m, KS& s) {
        survivor lane) + (its index), the order of the pass below -- no private (scratch) arrays */
     constexpr int NST = KS::NPST;
     static_assert(KS::BAIL && KS::MAXCON <= NST && NST <= 64, "compact narrowphase stage must hold MAXCON");
-    if constexpr (KS::MESHES) w_mesh_pass(m, s, nsurv);
+    if constexpr (KS::MESHES) {
+      w_mesh_pass(m, s, nsurv);
+      WT(48);
+    }
     auto& ch = s.kn.chunk();
     if (lane == 0) ch.np_nstage = 0;
     __builtin_amdgcn_wave_barrier();

@@ -382,8 +382,11 @@ class Batch:
         """{envs_per_cu, lds_bytes, regs, kernel} of the step kernel this handle launches"""
         e, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         self._chk(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
-        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value,
-                "kernel": self.SCHEDULES.get(self.L.ur3e_batch_schedule(self.h), "?")}
+        name = self.SCHEDULES.get(self.L.ur3e_batch_schedule(self.h), "?")
+        mc = self.model_c
+        if any(mc.geom_type[i] == 7 for i in range(mc.ngeom)):  # the mesh-capable tier set (KSS_NV_M, KSL_M)
+            name = name.replace("KSS_NV>", "KSS_NV_M>").replace("KSL>", "KSL_M>")
+        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value, "kernel": name}
 
     def set_timing(self, on: bool = True):
         """Record HIP events around every (uncaptured) step, for last_step_ms()."""
