@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-5 GPU call: VecNormalize statistics kernel (double-buffered, prefetched): parity and the C5 env path
+set -o pipefail
+R=$(pwd); D=$R/gpurun_out/$1; mkdir -p $D
+cd /tmp && export TMPDIR=/tmp; cd $R
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c5_policy.py -x -q -k "vecnorm or c5 or policy" --timeout 500 --timeout-method thread > $D/vn_tests.txt 2>&1 || { tail -40 $D/vn_tests.txt; exit 1; }
+tail -1 $D/vn_tests.txt
+timeout -k 10 120 python3 -u tools/vecnorm_trace.py 4096 64 > $D/vecnorm.txt 2>&1 || exit $?
+grep -v amdgpu.ids $D/vecnorm.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/vn_trace -o run -- python3 tools/vecnorm_trace.py 4096 64 > $D/vn_trace.log 2>&1 || exit $?
+grep -E "k_vn|Name" $D/vn_trace/run_kernel_stats.csv | cut -c1-160

@@ -32,7 +32,7 @@ names = {24: "load state+action+carry", 35: "controller (lane 0, substep 0)", 23
          39: "(r) collision: broadphase", 40: "(r) tree LDL' factor (smooth + Euler)",
          41: "(r) eval: J.qacc, M.qacc", 42: "(r) eval: constraint update", 43: "(r) eval: cost sums",
          44: "(r) grad: J'f", 45: "(r) ls eval: row terms", 46: "(r) ls eval: sums", 47: "(r) direction: cone Hessians",
-         48: "(r) collision: mesh pairs (wave GJK/EPA)"}
+         48: "(r) collision: mesh pairs (wave GJK/EPA)", 49: "(count only) mesh pairs settled by the wave"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 epb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 work = sys.argv[3] if len(sys.argv) > 3 else "gym"
@@ -48,7 +48,7 @@ if work == "gym":
                                     schedule=1), n)
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device="cuda")
-    for i in range(3):
+    for i in range(int(os.environ.get("UR3E_STAGE_PRE", "3"))):  # untimed env-steps from reset first
         b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
     K, subs = 5, 2
     steps = [lambda: b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))] * K
@@ -66,7 +66,7 @@ for f in steps:
     f()
 torch.cuda.synchronize()
 L.ur3e_debug_stage_cycles_tier(tier, cyc, calls, 1)
-tot = sum(cyc[k] for k in names if k != 28)
+tot = sum(cyc[k] for k in names if k not in (28, 49))
 units = calls[23] if calls[23] else 1  # forward passes run (substeps + retries + resets)
 print(f"tier {tier}, workload {work}: per-forward cycles (lane 0 view), {n} envs, {K} steps, "
       f"{calls[23]} forward passes in this tier")

@@ -296,8 +296,16 @@ UR3E_HD void ur3e_mink_support(const ur3e_cvx* A, const ur3e_cvx* B, const doubl
 }
 
 /* GJK: returns 1 on overlap (s holds a tetrahedron enclosing the origin, or a lower simplex touching
-   it), 0 when separated, with the closest points pa (on A) and pb (on B) */
-UR3E_HD int ur3e_gjk(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, double pa[3], double pb[3]) {
+   it), 0 when separated, with the closest points pa (on A) and pb (on B).
+   cut >= 0: returns 2 as soon as a support point proves the shapes farther apart than cut.  The new
+   support w = s_{A-B}(-v) bounds A - B by the plane {x : x.v >= w.v}, so dist(A, B) >= w.v / |v|; a caller
+   that only needs to know whether the distance exceeds a margin (every caller here: a pair farther apart
+   than its margin gives no contact) stops there instead of refining the closest points.  The exit also
+   keeps certainly-separated pairs away from the tetrahedron test below, which on a nearly flat simplex
+   could report the origin inside for hulls that are apart (round 5: two such pairs in the holding-pose
+   test, tests/test_gpu_mesh_main.py, gave EPA "contacts" with positive distance). */
+UR3E_HD int ur3e_gjk(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, double pa[3], double pb[3],
+                     double cut) {
   double d[3];
   ur3e_cvx_sub(d, B->pos, A->pos); /* initial direction: toward A - B's origin side */
   d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
@@ -313,8 +321,10 @@ UR3E_HD int ur3e_gjk(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, doub
     const double nd[3] = {-v[0], -v[1], -v[2]};
     double a[3], b[3], w[3];
     ur3e_mink_support(A, B, nd, a, b, w);
+    const double vw = ur3e_cvx_dot(v, w);
+    if (cut >= 0 && vw > 0 && vw * vw > cut * cut * vv) return 2; /* apart beyond cut */
     /* no progress toward the origin: v is the minimum distance vector */
-    if (vv - ur3e_cvx_dot(v, w) <= UR3E_GJK_TOL * vv) break;
+    if (vv - vw <= UR3E_GJK_TOL * vv) break;
     const int k = s->n;
     for (int c = 0; c < 3; c++) { s->w[k][c] = w[c]; s->a[k][c] = a[c]; s->b[k][c] = b[c]; }
     s->n = k + 1;
@@ -331,10 +341,15 @@ UR3E_HD int ur3e_gjk(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, doub
 /* ur3e_convex_convex's no-contact decision without EPA: 1 when GJK finds A and B apart by more than
    margin (or at zero distance, which reports nothing either), 0 when ur3e_convex_convex may report a
    contact (overlap, or a gap within the margin).  Same calls, same arithmetic as its GJK branch. */
+/* UR3E_GJK_CUT_SLACK: the certificate's slack over the margin, above the rounding of w.v (~1e-15 at
+   these scales) */
+#define UR3E_GJK_CUT_SLACK 1e-9
 UR3E_HD int ur3e_convex_separated(const ur3e_cvx* A, const ur3e_cvx* B, double margin) {
   ur3e_simplex s;
   double pa[3], pb[3];
-  if (ur3e_gjk(A, B, &s, pa, pb)) return 0;
+  const int g = ur3e_gjk(A, B, &s, pa, pb, margin + UR3E_GJK_CUT_SLACK);
+  if (g == 2) return 1;
+  if (g) return 0;
   double dv[3];
   ur3e_cvx_sub(dv, pb, pa);
   const double dd = sqrt(ur3e_cvx_dot(dv, dv));
@@ -499,7 +514,9 @@ UR3E_HD int ur3e_convex_convex(const ur3e_cvx* A, const ur3e_cvx* B, double marg
                                double pos[3], double nrm[3], double* dist) {
   ur3e_simplex s;
   double pa[3], pb[3];
-  if (!ur3e_gjk(A, B, &s, pa, pb)) {
+  const int g = ur3e_gjk(A, B, &s, pa, pb, margin + UR3E_GJK_CUT_SLACK);
+  if (g == 2) return 0; /* apart beyond the margin: no contact */
+  if (!g) {
     double dv[3];
     ur3e_cvx_sub(dv, pb, pa);
     const double dd = sqrt(ur3e_cvx_dot(dv, dv));

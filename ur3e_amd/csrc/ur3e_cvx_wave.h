@@ -427,9 +427,9 @@ WD int wc_closest(WCvxWork& W, double v[3]) {
   return 0;
 }
 
-/* ur3e_gjk: 1 on overlap (the simplex in W), 0 when separated, with the closest points pa, pb */
+/* ur3e_gjk (convex.h, the same early exit: 2 when a support point proves the hulls farther apart than cut) */
 WD int wc_gjk(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const WCvxLane& lb, WCvxWork& W,
-              double pa[3], double pb[3]) {
+              double pa[3], double pb[3], double cut = -1.0) {
   double d[3];
   ur3e_cvx_sub(d, B.pos, A.pos);
   d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
@@ -448,7 +448,9 @@ WD int wc_gjk(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const 
     if (vv <= 1e-30) return 1;
     const double nd[3] = {-v[0], -v[1], -v[2]};
     wc_mink(A, la, B, lb, nd, a, b, w);
-    if (vv - ur3e_cvx_dot(v, w) <= UR3E_GJK_TOL * vv) break;
+    const double vw = ur3e_cvx_dot(v, w);
+    if (cut >= 0 && vw > 0 && vw * vw > cut * cut * vv) return 2; /* apart beyond cut */
+    if (vv - vw <= UR3E_GJK_TOL * vv) break;
     const int k = W.sn;
 #pragma unroll
     for (int c = 0; c < 3; c++) { W.sw[k][c] = w[c]; W.sa[k][c] = a[c]; W.sb[k][c] = b[c]; }
@@ -470,7 +472,9 @@ WD int wc_gjk(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const 
 WD bool wc_convex_separated(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const WCvxLane& lb,
                             WCvxWork& W, double margin) {
   double pa[3], pb[3];
-  if (wc_gjk(A, la, B, lb, W, pa, pb)) return false;
+  const int g = wc_gjk(A, la, B, lb, W, pa, pb, margin + UR3E_GJK_CUT_SLACK);
+  if (g == 2) return true;
+  if (g) return false;
   double dv[3];
   ur3e_cvx_sub(dv, pb, pa);
   const double dd = sqrt(ur3e_cvx_dot(dv, dv));
@@ -741,7 +745,9 @@ WD int wc_epa(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const 
 WD int wc_convex_convex(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const WCvxLane& lb,
                         WCvxWork& W, double margin, double* res) {
   double pa[3], pb[3];
-  if (!wc_gjk(A, la, B, lb, W, pa, pb)) {
+  const int g = wc_gjk(A, la, B, lb, W, pa, pb, margin + UR3E_GJK_CUT_SLACK);
+  if (g == 2) return 0; /* apart beyond the margin: convex.h's no-contact answer */
+  if (!g) {
     double dv[3];
     ur3e_cvx_sub(dv, pb, pa);
     const double dd = sqrt(ur3e_cvx_dot(dv, dv));

@@ -1070,6 +1070,9 @@ WD void w_mesh_pass(KModel m, KS& s, int nsurv) {
     const int q = __builtin_ctzll(bm);
     bm &= bm - 1;
     const int pq = rli(p, q);
+#ifdef UR3E_STAGE_TIMING
+    if (lane == 0) s.tcnt[49] += 1; /* diagnostic: mesh pairs settled by the wave */
+#endif
     const int g1 = m->cpair_geom1[pq], g2 = m->cpair_geom2[pq];
     const double margin = m->cpair_margin[pq];
     WCvxShape B;
