@@ -1,11 +1,12 @@
 /* On-device SB3 VecNormalize (include/ur3e_vecnorm.h): running observation / return statistics in
  * numpy's exact reduction order, then normalisation.
  *
- * k_vn_stats (two workgroups of 1024 threads on two CUs, rows staged through LDS):
- *   block 1: returns = returns * gamma + reward (all threads), then thread 0 runs numpy's pairwise
- *     summation (8 accumulators per <=128 block, halves rounded down to multiples of 8) over each
- *     8192-element buffer, the buffer sums added in order, for the 1-D mean and var of the returns;
- *   block 0, thread j < dim: column j of obs [n, dim]: mean = (((x0 + x1) + x2) + ...) / n and
+ * k_vn_stats (dim + 1 workgroups of 1024 threads, one per observation column and one for the returns):
+ *   workgroup dim: returns = returns * gamma + reward (all threads), then numpy's pairwise summation
+ *     (8 accumulators per <=128 block, halves rounded down to multiples of 8) over each 8192-element
+ *     buffer, leaves on separate threads, the tree and the buffer sums added in numpy's order, for the
+ *     1-D mean and var of the returns;
+ *   workgroup j < dim: column j of obs [n, dim]: mean = (((x0 + x1) + x2) + ...) / n and
  *     var = sum((x - mean)^2) / n in the same row-sequential order numpy uses for an axis-0
  *     reduction of a C-contiguous array, then RunningMeanStd.update_from_moments.
  * k_vn_apply (n x dim threads): obs / terminal-obs normalisation to f32, reward normalisation,
@@ -25,60 +26,31 @@ int ur3e_internal_fail(int code, const char* msg);
     if (_e != hipSuccess) return ur3e_internal_fail(UR3E_EHIP, hipGetErrorString(_e)); \
   } while (0)
 
-/* numpy pairwise_sum over a contiguous double array (numpy/_core/src/umath/loops_utils.h.src), of
-   the values f(a[i]): blocks < 8 sum sequentially from 0.0, blocks <= 128 use 8 strided accumulators
-   combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail, larger blocks split at
-   n/2 rounded down to a multiple of 8.  The recursion runs on an explicit stack.  P is an LDS- or
-   global-address-space pointer: through a generic pointer every load of this serial chain would be
-   a FLAT load (LDS data at FLAT latency, and every wait counting both memory counters). */
+/* numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) over a contiguous double array, of the
+   values f(a[i]): blocks < 8 sum sequentially from 0.0, blocks <= 128 use 8 strided accumulators
+   combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail, larger blocks split at n/2 rounded
+   down to a multiple of 8.  vn_leaf is a block of <= 128; vn_sum_par below lays out the splits.  P is an
+   LDS- or global-address-space pointer: through a generic pointer every load of these serial chains
+   would be a FLAT load (LDS data at FLAT latency, and every wait counting both memory counters). */
 typedef const __attribute__((address_space(3))) double* VnLds;
 typedef const __attribute__((address_space(1))) double* VnGlobal;
 template <class P, class F>
-__device__ static double vn_pairwise(P a, int n, F f) {
-  struct Fr { int off, len, stage; double left; };
-  Fr stk[32];
-  int sp = 0;
-  stk[0] = {0, n, 0, 0.0};
-  double ret = 0.0;
-  for (;;) {
-    Fr& fr = stk[sp];
-    if (fr.stage == 0) {
-      if (fr.len < 8) {
-        double res = 0.0;
-        for (int i = 0; i < fr.len; i++) res += f(a[fr.off + i]);
-        ret = res;
-      } else if (fr.len <= 128) {
-        double r[8];
-        for (int j = 0; j < 8; j++) r[j] = f(a[fr.off + j]);
-        int i;
-        for (i = 8; i < fr.len - (fr.len % 8); i += 8)
-          for (int j = 0; j < 8; j++) r[j] += f(a[fr.off + i + j]);
-        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < fr.len; i++) res += f(a[fr.off + i]);
-        ret = res;
-      } else {
-        int n2 = fr.len / 2;
-        n2 -= n2 % 8;
-        fr.stage = 1;
-        stk[sp + 1] = {fr.off, n2, 0, 0.0};
-        sp++;
-        continue;
-      }
-    } else if (fr.stage == 1) {
-      /* left half is in ret: descend into the right half */
-      int n2 = fr.len / 2;
-      n2 -= n2 % 8;
-      fr.left = ret;
-      fr.stage = 2;
-      stk[sp + 1] = {fr.off + n2, fr.len - n2, 0, 0.0};
-      sp++;
-      continue;
-    } else {
-      ret = fr.left + ret;
-    }
-    if (sp == 0) return ret;
-    sp--;
+__device__ static double vn_leaf(P a, int len, F f) {
+  if (len < 8) {
+    double res = 0.0;
+    for (int i = 0; i < len; i++) res += f(a[i]);
+    return res;
   }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) r[j] = f(a[j]);
+  int i;
+  for (i = 8; i < len - (len % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] += f(a[i + j]);
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < len; i++) res += f(a[i]);
+  return res;
 }
 
 /* a 1-D np.sum / np.mean of a contiguous double array: numpy's reduction iterator hands the add loop
@@ -86,10 +58,59 @@ __device__ static double vn_pairwise(P a, int n, F f) {
    order, starting from the additive identity -- for n > 8192 a single whole-array pairwise sum would
    round differently */
 #define VN_NP_BUFSIZE 8192
+
+/* The same 1-D sum with the whole workgroup: numpy's pairwise recursion over each 8192-element buffer is laid
+   out as a node list (thread 0, children after their parent: a node longer than 128 splits at half its
+   length rounded down to a multiple of 8), every leaf (<= 128 elements) is summed by its own thread with
+   numpy's leaf code (vn_leaf), and thread 0 adds each internal node's
+   children left + right, children first -- the same additions in the same tree as the serial recursion,
+   without its frame stack in private memory (round 5: 174 us of the 180 us statistics kernel at 4,096
+   envs were that stack's walk on one thread). */
+#define VN_MAXNODE 256 /* a tree over <= 8192 elements has <= 255 nodes (leaves hold >= 64) */
+struct VnTree {
+  int off[VN_MAXNODE], len[VN_MAXNODE], left[VN_MAXNODE];
+  double val[VN_MAXNODE];
+  int nn;
+};
 template <class P, class F>
-__device__ static double vn_sum(P a, int n, F f) {
+__device__ static double vn_sum_par(VnTree& t, P a, int n, F f) {
+  const int tid = threadIdx.x;
   double res = 0.0;
-  for (int b = 0; b < n; b += VN_NP_BUFSIZE) res = res + vn_pairwise(a + b, n - b < VN_NP_BUFSIZE ? n - b : VN_NP_BUFSIZE, f);
+  for (int b = 0; b < n; b += VN_NP_BUFSIZE) {
+    const int len = n - b < VN_NP_BUFSIZE ? n - b : VN_NP_BUFSIZE;
+    __syncthreads();
+    if (tid == 0) {
+      t.off[0] = b;
+      t.len[0] = len;
+      int nn = 1;
+      for (int k = 0; k < nn; k++) {
+        const int l = t.len[k];
+        if (l <= 128) {
+          t.left[k] = -1;
+          continue;
+        }
+        int n2 = l / 2;
+        n2 -= n2 % 8;
+        t.left[k] = nn;
+        t.off[nn] = t.off[k]; t.len[nn] = n2;
+        t.off[nn + 1] = t.off[k] + n2; t.len[nn + 1] = l - n2;
+        nn += 2;
+      }
+      t.nn = nn;
+    }
+    __syncthreads();
+    const int nn = t.nn;
+    for (int k = tid; k < nn; k += blockDim.x)
+      if (t.left[k] < 0) t.val[k] = vn_leaf(a + t.off[k], t.len[k], f);
+    __syncthreads();
+    if (tid == 0) {
+      for (int k = nn - 1; k >= 0; k--)
+        if (t.left[k] >= 0) t.val[k] = t.val[t.left[k]] + t.val[t.left[k] + 1];
+      t.val[0] = res + t.val[0];
+    }
+    __syncthreads();
+    res = t.val[0];
+  }
   return res;
 }
 
@@ -108,93 +129,114 @@ __device__ static void vn_moments(double* mean, double* var, double c, double bm
   *var = new_var;
 }
 
-/* One workgroup of VN_NT threads.  The serial orders are fixed by numpy, so the work here is keeping
-   the loads off the dependent add chains: the whole workgroup stages row chunks of obs (and the
-   returns) into LDS with coalesced loads, then the lanes that own a column (obs) or lane 0
-   (returns, pairwise) walk LDS in numpy's order. */
+/* dim + 1 workgroups of VN_NT threads.  The serial orders are fixed by numpy, so the work is keeping
+   everything but the dependent additions off the chains.  Workgroup j < dim owns observation column j
+   and runs it on its first wave with the column in REGISTERS: lane k holds VN_RPL consecutive rows of
+   each 64 * VN_RPL-row round, and the chain visits the lanes in order -- lane k adds its rows (a run of
+   dependent adds with register operands, no memory access on the chain) and hands the running sum to
+   lane k + 1 by readlane.  Both sweeps (sum; then the squared deviations from the batch mean, formed on
+   all lanes at once before the chain) load the column once each.  Workgroup dim owns the returns (1-D,
+   numpy's pairwise tree, vn_sum_par).  The columns run on separate CUs at once; the new observation
+   count (shared by every column) is stored by k_vn_apply, after every column has read the old one.
+   Round 5: one workgroup walking all 24 columns through restaged LDS chunks took 126 us at 4,096 envs;
+   chains over LDS, 81 us (bound by the reads' latency); in registers, see DESIGN.md section 7. */
 #define VN_NT 1024
-#define VN_LDS_DOUBLES 12288 /* 96 KB of obs rows per chunk */
+#define VN_RPL 32            /* rows per lane per round (64 VGPRs: the 1,024-thread bound allows 128) */
 #define VN_RET_LDS 4096      /* returns staged in LDS when n <= this (32 KB) */
+
+__device__ __forceinline__ double vn_rl(double v, int lane) {
+  long long b = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), lane);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+/* one sweep of column j (wave 0): PASS 0 returns x0 + x1 + ... (row order), PASS 1 d0^2 + d1^2 + ...
+   with d = x - bm; the first term starts the sum (numpy's reduction has no identity there) */
+template <int PASS>
+__device__ static double vn_column(const double* __restrict__ obs, int n, int dim, int j, double bm) {
+  const int lane = threadIdx.x;
+  double s = 0.0;
+  for (int base = 0; base < n; base += 64 * VN_RPL) {
+    double v[VN_RPL];
+#pragma unroll
+    for (int r = 0; r < VN_RPL; r++) {
+      const int row = base + lane * VN_RPL + r;
+      const double x = row < n ? obs[(size_t)row * dim + j] : 0.0;
+      if (PASS == 0) {
+        v[r] = x;
+      } else {
+        const double d = x - bm;
+        v[r] = d * d;
+      }
+    }
+    for (int t = 0; t < 64; t++) {
+      const int row0 = base + t * VN_RPL;
+      if (row0 >= n) break;
+      const int cnt = n - row0 < VN_RPL ? n - row0 : VN_RPL;
+      if (lane == t) {
+        double acc = row0 == 0 ? v[0] : s + v[0];
+        if (cnt == VN_RPL) {
+#pragma unroll
+          for (int r = 1; r < VN_RPL; r++) acc = acc + v[r];
+        } else {
+#pragma unroll
+          for (int r = 1; r < VN_RPL; r++)
+            if (r < cnt) acc = acc + v[r];
+        }
+        s = acc;
+      }
+      s = vn_rl(s, t);
+    }
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(VN_NT) void k_vn_stats(ur3e_vecnorm_stats_t st, int n, int dim,
                                                     const double* __restrict__ obs, const double* __restrict__ rew,
                                                     int upd_obs, int upd_ret, double gamma, int reset) {
-  __shared__ double buf[VN_LDS_DOUBLES];
   __shared__ double rbuf[VN_RET_LDS];
+  __shared__ VnTree tree;
   const int tid = threadIdx.x;
   const double bn = (double)n;
-  /* block 1: discounted returns and their statistics (1-D: numpy pairwise summation); block 0: the
-     observation columns -- independent, so they run on two CUs at once */
-  if (blockIdx.x == 1) {
-  if (reset) {
-    for (int i = tid; i < n; i += VN_NT) st.returns[i] = 0.0;
-  } else if (upd_ret) {
-    const bool in_lds = n <= VN_RET_LDS;
-    for (int i = tid; i < n; i += VN_NT) {
-      const double r = st.returns[i] * gamma + rew[i];
-      st.returns[i] = r;
-      if (in_lds) rbuf[i] = r;
-    }
-    __threadfence_block();
-    __syncthreads();
-    if (tid == 0) {
+  if ((int)blockIdx.x == dim) {
+    /* the discounted returns and their statistics (1-D: numpy pairwise summation) */
+    if (reset) {
+      for (int i = tid; i < n; i += VN_NT) st.returns[i] = 0.0;
+    } else if (upd_ret) {
+      const bool in_lds = n <= VN_RET_LDS;
+      for (int i = tid; i < n; i += VN_NT) {
+        const double r = st.returns[i] * gamma + rew[i];
+        st.returns[i] = r;
+        if (in_lds) rbuf[i] = r;
+      }
+      __threadfence_block();
+      __syncthreads();
       double bm, q;
       if (in_lds) {
         const VnLds a = (VnLds)rbuf;
-        bm = vn_sum(a, n, [](double x) { return x; }) / bn;
-        q = vn_sum(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+        bm = vn_sum_par(tree, a, n, [](double x) { return x; }) / bn;
+        q = vn_sum_par(tree, a, n, [bm](double x) { const double d = x - bm; return d * d; });
       } else {
         const VnGlobal a = (VnGlobal)st.returns;
-        bm = vn_sum(a, n, [](double x) { return x; }) / bn;
-        q = vn_sum(a, n, [bm](double x) { const double d = x - bm; return d * d; });
+        bm = vn_sum_par(tree, a, n, [](double x) { return x; }) / bn;
+        q = vn_sum_par(tree, a, n, [bm](double x) { const double d = x - bm; return d * d; });
       }
-      const double c = *st.ret_count;
-      vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);
-      *st.ret_count = bn + c;
+      if (tid == 0) {
+        const double c = *st.ret_count;
+        vn_moments(st.ret_mean, st.ret_var, c, bm, q / bn, bn);
+        *st.ret_count = bn + c;
+      }
     }
-  }
-  return;
+    return;
   }
   if (!upd_obs) return;
-  /* ---- observation columns: np.mean / np.var over axis 0 of a C-contiguous [n, dim], row-sequential
-     per column; two sweeps (sum, then squared deviations from the batch mean) ---- */
-  const int rows = VN_LDS_DOUBLES / dim;
-  const int j = tid;
-  double s = 0.0, bm = 0.0, q = 0.0;
-  for (int pass = 0; pass < 2; pass++) {
-    for (int base = 0; base < n; base += rows) {
-      const int nr = n - base < rows ? n - base : rows;
-      __syncthreads();
-      const size_t off = (size_t)base * dim;
-      for (int k = tid; k < nr * dim; k += VN_NT) buf[k] = obs[off + k];
-      __syncthreads();
-      if (j < dim) {
-        int i0 = 0;
-        if (base == 0) { /* numpy starts each column from its first element */
-          if (pass == 0) {
-            s = buf[j];
-          } else {
-            const double d0 = buf[j] - bm;
-            q = d0 * d0;
-          }
-          i0 = 1;
-        }
-        if (pass == 0) {
-#pragma unroll 8
-          for (int i = i0; i < nr; i++) s = s + buf[i * dim + j];
-        } else {
-#pragma unroll 8
-          for (int i = i0; i < nr; i++) {
-            const double d = buf[i * dim + j] - bm;
-            q = q + d * d;
-          }
-        }
-      }
-    }
-    if (pass == 0) bm = s / bn;
-  }
-  if (j < dim) vn_moments(st.obs_mean + j, st.obs_var + j, *st.obs_count, bm, q / bn, bn);
-  __syncthreads(); /* every column read the old count before it is replaced */
-  if (tid == 0) *st.obs_count = bn + *st.obs_count;
+  /* ---- observation column j: np.mean / np.var over axis 0 of a C-contiguous [n, dim], row-sequential ---- */
+  if (tid >= 64) return;
+  const int j = blockIdx.x;
+  const double bm = vn_column<0>(obs, n, dim, j, 0.0) / bn;
+  const double q = vn_column<1>(obs, n, dim, j, bm);
+  if (tid == 0) vn_moments(st.obs_mean + j, st.obs_var + j, *st.obs_count, bm, q / bn, bn);
 }
 
 __device__ static inline float vn_norm(double x, double mean, double var, double eps, double clip) {
@@ -208,9 +250,11 @@ __global__ void k_vn_apply(ur3e_vecnorm_stats_t st, int n, int dim, const double
                            const double* __restrict__ rew, const unsigned char* __restrict__ term,
                            const unsigned char* __restrict__ trunc, const double* __restrict__ tobs, int norm_obs,
                            int norm_reward, double clip_obs, double clip_reward, double eps, float* __restrict__ obs_out,
-                           double* __restrict__ rew_out, float* __restrict__ tobs_out) {
+                           double* __restrict__ rew_out, float* __restrict__ tobs_out, int upd_count) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n * dim) return;
+  /* the observation count of the statistics k_vn_stats just updated (every column read the old one) */
+  if (upd_count && k == 0) *st.obs_count = (double)n + *st.obs_count;
   const int i = k / dim, j = k - i * dim;
   const bool done = term && trunc && (term[i] || trunc[i]);
   if (norm_obs && obs_out) {
@@ -249,12 +293,13 @@ extern "C" int ur3e_vecnorm_step(const ur3e_vecnorm_stats_t* st, const ur3e_vecn
   if (rc) return rc;
   if (!d_rew || !d_term || !d_trunc) return ur3e_internal_fail(UR3E_EINVAL, "null reward / done buffer");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_vn_stats, dim3(2), dim3(VN_NT), 0, s, *st, n, dim, d_obs, d_rew, cfg->training && cfg->norm_obs,
-                     cfg->training, cfg->gamma, 0);
+  const int upd_obs = cfg->training && cfg->norm_obs;
+  hipLaunchKernelGGL(k_vn_stats, dim3(dim + 1), dim3(VN_NT), 0, s, *st, n, dim, d_obs, d_rew, upd_obs, cfg->training,
+                     cfg->gamma, 0);
   VN_CHK(hipGetLastError());
   hipLaunchKernelGGL(k_vn_apply, dim3((n * dim + 255) / 256), dim3(256), 0, s, *st, n, dim, d_obs, d_rew, d_term,
                      d_trunc, d_tobs, cfg->norm_obs, cfg->norm_reward, cfg->clip_obs, cfg->clip_reward, cfg->epsilon,
-                     d_obs_out, d_rew_out, d_tobs_out);
+                     d_obs_out, d_rew_out, d_tobs_out, upd_obs);
   VN_CHK(hipGetLastError());
   return UR3E_OK;
 }
@@ -264,11 +309,12 @@ extern "C" int ur3e_vecnorm_reset(const ur3e_vecnorm_stats_t* st, const ur3e_vec
   int rc = vn_check(st, cfg, n, dim, d_obs);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_vn_stats, dim3(2), dim3(VN_NT), 0, s, *st, n, dim, d_obs, nullptr, cfg->training && cfg->norm_obs,
-                     0, cfg->gamma, 1);
+  const int upd_obs = cfg->training && cfg->norm_obs;
+  hipLaunchKernelGGL(k_vn_stats, dim3(dim + 1), dim3(VN_NT), 0, s, *st, n, dim, d_obs, nullptr, upd_obs, 0, cfg->gamma, 1);
   VN_CHK(hipGetLastError());
   hipLaunchKernelGGL(k_vn_apply, dim3((n * dim + 255) / 256), dim3(256), 0, s, *st, n, dim, d_obs, nullptr, nullptr,
-                     nullptr, nullptr, cfg->norm_obs, 0, cfg->clip_obs, 0.0, cfg->epsilon, d_obs_out, nullptr, nullptr);
+                     nullptr, nullptr, cfg->norm_obs, 0, cfg->clip_obs, 0.0, cfg->epsilon, d_obs_out, nullptr, nullptr,
+                     upd_obs);
   VN_CHK(hipGetLastError());
   return UR3E_OK;
 }
@@ -280,7 +326,7 @@ extern "C" int ur3e_vecnorm_normalize_obs(const ur3e_vecnorm_stats_t* st, const 
   if (!d_obs_out) return ur3e_internal_fail(UR3E_EINVAL, "null output");
   hipLaunchKernelGGL(k_vn_apply, dim3((n * dim + 255) / 256), dim3(256), 0, (hipStream_t)stream, *st, n, dim, d_obs,
                      nullptr, nullptr, nullptr, nullptr, 1, 0, cfg->clip_obs, 0.0, cfg->epsilon, d_obs_out, nullptr,
-                     nullptr);
+                     nullptr, 0);
   VN_CHK(hipGetLastError());
   return UR3E_OK;
 }
