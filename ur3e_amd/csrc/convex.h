@@ -82,27 +82,6 @@ UR3E_HD void ur3e_cvx_support(const ur3e_cvx* c, const double d[3], double out[3
 }
 
 /* ---- plane (geom1: normal = z axis of its frame) vs convex hull (geom2) --------------------- */
-/* ur3e_plane_convex's no-contact decision: 1 when every vertex lies beyond the margin (the same signed
-   distances, the same test), so that it would return 0 */
-UR3E_HD int ur3e_plane_convex_clear(const double pp[3], const double pm[9], const ur3e_cvx* c, double margin) {
-  const double n[3] = {pm[2], pm[5], pm[8]};
-  double dif[3];
-  ur3e_cvx_sub(dif, c->pos, pp);
-  const double d0 = ur3e_cvx_dot(n, dif);
-  const double* R = c->mat;
-  int clear = 1;
-  for (int k = 0; k < c->nv; k++) {
-    const double* v = c->v + 3 * k;
-    double w[3];
-    w[0] = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
-    w[1] = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
-    w[2] = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
-    const double dd = d0 + ur3e_cvx_dot(n, w);
-    if (!(dd > margin)) clear = 0;
-  }
-  return clear;
-}
-
 UR3E_HD int ur3e_plane_convex(const double pp[3], const double pm[9], const ur3e_cvx* c, double margin,
                               double pos[][3], double nrm[][3], double* dist) {
   const double n[3] = {pm[2], pm[5], pm[8]};
@@ -338,23 +317,9 @@ UR3E_HD int ur3e_gjk(const ur3e_cvx* A, const ur3e_cvx* B, ur3e_simplex* s, doub
   return 0;
 }
 
-/* ur3e_convex_convex's no-contact decision without EPA: 1 when GJK finds A and B apart by more than
-   margin (or at zero distance, which reports nothing either), 0 when ur3e_convex_convex may report a
-   contact (overlap, or a gap within the margin).  Same calls, same arithmetic as its GJK branch. */
-/* UR3E_GJK_CUT_SLACK: the certificate's slack over the margin, above the rounding of w.v (~1e-15 at
-   these scales) */
+/* UR3E_GJK_CUT_SLACK: the separating-axis certificate's slack over the margin, above the rounding of
+   w.v (~1e-15 at these scales) */
 #define UR3E_GJK_CUT_SLACK 1e-9
-UR3E_HD int ur3e_convex_separated(const ur3e_cvx* A, const ur3e_cvx* B, double margin) {
-  ur3e_simplex s;
-  double pa[3], pb[3];
-  const int g = ur3e_gjk(A, B, &s, pa, pb, margin + UR3E_GJK_CUT_SLACK);
-  if (g == 2) return 1;
-  if (g) return 0;
-  double dv[3];
-  ur3e_cvx_sub(dv, pb, pa);
-  const double dd = sqrt(ur3e_cvx_dot(dv, dv));
-  return !(dd <= margin) || !(dd > 0);
-}
 
 /* ---- EPA: penetration of overlapping A, B from a GJK simplex --------------------------------- */
 typedef struct {

@@ -159,27 +159,6 @@ WD double wc_plane_dist(const double n[3], double d0, const WCvxShape& c, double
   return d0 + ur3e_cvx_dot(n, w);
 }
 
-/* ur3e_plane_convex_clear */
-WD bool wc_plane_convex_clear(const double pp[3], const double pm[9], const WCvxShape& c, const WCvxLane& lv,
-                              double margin) {
-  const double n[3] = {pm[2], pm[5], pm[8]};
-  double dif[3];
-  ur3e_cvx_sub(dif, c.pos, pp);
-  const double d0 = ur3e_cvx_dot(n, dif);
-  const int lane = w_lane();
-  bool near = false;
-  for (int base = 0; base < c.nv; base += 64) {
-    const int k = base + lane;
-    if (k < c.nv) {
-      double x = lv.x, y = lv.y, z = lv.z;
-      if (base) { x = c.v[3 * k]; y = c.v[3 * k + 1]; z = c.v[3 * k + 2]; }
-      const double dd = wc_plane_dist(n, d0, c, x, y, z);
-      near |= !(dd > margin);
-    }
-  }
-  return __ballot(near) == 0;
-}
-
 /* ur3e_plane_convex: up to UR3E_CVX_PLANE_MAX contacts into res (count returned) */
 WD int wc_plane_convex(const double pp[3], const double pm[9], const WCvxShape& c, const WCvxLane& lv,
                        double margin, WCvxWork& W, double (*res)[7], int room) {
@@ -466,19 +445,6 @@ WD int wc_gjk(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const 
     pa[c] = xa; pb[c] = xb;
   }
   return 0;
-}
-
-/* ur3e_convex_separated */
-WD bool wc_convex_separated(const WCvxShape& A, const WCvxLane& la, const WCvxShape& B, const WCvxLane& lb,
-                            WCvxWork& W, double margin) {
-  double pa[3], pb[3];
-  const int g = wc_gjk(A, la, B, lb, W, pa, pb, margin + UR3E_GJK_CUT_SLACK);
-  if (g == 2) return true;
-  if (g) return false;
-  double dv[3];
-  ur3e_cvx_sub(dv, pb, pa);
-  const double dd = sqrt(ur3e_cvx_dot(dv, dv));
-  return !(dd <= margin) || !(dd > 0);
 }
 
 /* ---- EPA (polytope in LDS, per-face work lane-parallel) ------------------------------------- */

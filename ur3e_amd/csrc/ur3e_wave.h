@@ -849,7 +849,7 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_MESH) {
     /* every hull vertex lies within geom_rbound of the geom's origin (the compiler's bound over the
        same vertices), so the centre beyond the margin by more than rbound + 1e-9 keeps every vertex
-       distance of ur3e_plane_convex_clear above the margin: the pair is clear */
+       distance of ur3e_plane_convex above the margin: the pair gives no contact */
     const double* pm = s.geom_xmat[g1];
     const double n[3] = {pm[2], pm[5], pm[8]};
     const double dif[3] = {s.geom_xpos[g2][0] - s.geom_xpos[g1][0], s.geom_xpos[g2][1] - s.geom_xpos[g1][1],
@@ -874,8 +874,8 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
   if (t1 != UR3E_GEOM_BOX && !mesh1) return false;
   /* box-box: k_box_box_t's own decision (> margin).  A convex mesh lies inside its geom_size box (the
      compiler's half extents of the same hull vertices), so two shapes whose boxes separate by more than
-     the margin + 1e-6 along a face axis are apart beyond the margin: GJK (ur3e_convex_separated /
-     the full tier's GJK + EPA) finds no contact for them, to well within that 1e-6 */
+     the margin + 1e-6 along a face axis are apart beyond the margin: GJK (the wavefront's or the full
+     tier's) finds no contact for them, to well within that 1e-6 */
   const double lim = (mesh1 || mesh2) ? margin + 1e-6 : margin;
   const double* R1 = s.geom_xmat[g1];
   const double* R2 = s.geom_xmat[g2];
@@ -940,17 +940,6 @@ __device__ __forceinline__ int w_mesh_collide(KModel m, const KS& s, int g1, int
   w_geom_convex(m, s, g1, &a);
   ur3e_epa scratch;
   return ur3e_convex_convex(&a, &b, margin, &scratch, raw[0].pos, raw[0].n, &raw[0].dist);
-}
-
-/* the mesh pair (g1, g2) reports no contact (ur3e_plane_convex_clear / ur3e_convex_separated) */
-template <class KS>
-__device__ __forceinline__ bool w_mesh_separated(KModel m, const KS& s, int g1, int g2, double margin) {
-  ur3e_cvx b;
-  w_geom_convex(m, s, g2, &b);
-  if (m->geom_type[g1] == UR3E_GEOM_PLANE) return ur3e_plane_convex_clear(s.geom_xpos[g1], s.geom_xmat[g1], &b, margin);
-  ur3e_cvx a;
-  w_geom_convex(m, s, g1, &a);
-  return ur3e_convex_separated(&a, &b, margin);
 }
 
 /* narrowphase of candidate pair p (after w_pair_near): raw contacts, returns their count */
