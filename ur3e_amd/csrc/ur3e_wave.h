@@ -1120,9 +1120,22 @@ WD void w_store_contact(KModel m, KS& s, int c, int p, const KRaw& r) {
    candidate order (ballot + mbcnt), ONE narrowphase per survivor (lane = survivor), contact
    offsets by a wave prefix scan of the counts, contacts written from the lane's own results.
    Same contacts in the same order as the count / prefix / write passes of w_collision. */
+/* the bounding-sphere survivors' list of the overlaid layouts' two-pass broadphase (r_collision): the
+   narrowphase area's clip buffers, which are dead until the narrowphase (KS::NCAND ints <= 1 KB) */
+template <class KS>
+__device__ __forceinline__ int* w_near_list(KS& s) {
+  static_assert(sizeof(s.kn.chunk().np_clip) >= KS::NCAND * sizeof(int), "near list exceeds the clip buffers");
+  return reinterpret_cast<int*>(&s.kn.chunk().np_clip[0][0][0][0]);
+}
 /* the exact pre-narrowphase cull (w_pair_apart) on (1, default) or off (0: A/B) */
 #ifndef W_PAIR_CULL
 #define W_PAIR_CULL 1
+#endif
+/* the mesh-capable overlaid layouts' two-pass broadphase (1, default) or the single fused pass (0: A/B).
+   Measured (profiles/r05_ab, A/B 2): +0.5 % on the mesh model (234 candidates, four sphere passes), -1 % on
+   the box surrogate (92 candidates, two passes), which keeps the fused pass */
+#ifndef W_BROAD_2PASS
+#define W_BROAD_2PASS 1
 #endif
 template <class KS>
 WD void r_collision(KModel m, KS& s) {
@@ -1132,13 +1145,43 @@ WD void r_collision(KModel m, KS& s) {
   /* the overlaid layouts list W_MAXSURV survivors (an env-step with more hands on); the full-capacity
      layout every candidate */
   constexpr int CAP = KS::OVERLAY ? W_MAXSURV : KS::NCAND;
-  for (int base = 0; base < np; base += 64) {
-    const int p = base + lane;
-    const bool ok = p < np && w_pair_near(m, s, p) && !(W_PAIR_CULL && w_pair_apart(m, s, p));
-    const unsigned long long bm = __ballot(ok);
-    const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
-    if (ok && at < CAP) s.cand_off[at] = p;
-    nsurv += __popcll(bm);
+  if constexpr (KS::OVERLAY && KS::MESHES && W_PAIR_CULL && W_BROAD_2PASS) {
+    /* two compacted passes: the bounding-sphere test over every candidate (64 per pass), its survivors
+       listed in candidate order in the narrowphase area (dead until the narrowphase); then the exact cull
+       over that list only -- one pass for the sphere survivors instead of one per 64 candidates, whose
+       few surviving lanes would run the separating-axis test in every pass */
+    int* near = w_near_list(s);
+    constexpr int NCAP = KS::NCAND;
+    int nnear = 0;
+    for (int base = 0; base < np; base += 64) {
+      const int p = base + lane;
+      const bool ok = p < np && w_pair_near(m, s, p);
+      const unsigned long long bm = __ballot(ok);
+      const int at = nnear + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (ok && at < NCAP) near[at] = p;
+      nnear += __popcll(bm);
+    }
+    if (nnear > NCAP) nnear = NCAP; /* np <= KS::NCAND (the host checks ncpair): never taken */
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    for (int base = 0; base < nnear; base += 64) {
+      const int k = base + lane;
+      const int p = k < nnear ? near[k] : 0;
+      const bool ok = k < nnear && !w_pair_apart(m, s, p);
+      const unsigned long long bm = __ballot(ok);
+      const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (ok && at < CAP) s.cand_off[at] = p;
+      nsurv += __popcll(bm);
+    }
+  } else {
+    for (int base = 0; base < np; base += 64) {
+      const int p = base + lane;
+      const bool ok = p < np && w_pair_near(m, s, p) && !(W_PAIR_CULL && w_pair_apart(m, s, p));
+      const unsigned long long bm = __ballot(ok);
+      const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (ok && at < CAP) s.cand_off[at] = p;
+      nsurv += __popcll(bm);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
