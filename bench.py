@@ -243,7 +243,7 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
     return base, parity
 
 
-def other_configs(n_envs=4096, steps=50, warmup=5):
+def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500):
     """Throughput of the BASELINE configs other than the headline one, on one GPU (rank 0, N=1):
     C2 -- ur3e_2f85, random joint targets through move_j's PD (one mj_step per control step);
     C3 -- main.xml move_l_mug scripted pick (pid_task_ctrl along build_traj_l_pick_place rows,
@@ -291,16 +291,17 @@ def other_configs(n_envs=4096, steps=50, warmup=5):
     bm = rt.Batch(mc_m, cfg_m, n_envs)
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
-    acts_m = lo + (hi - lo) * torch.rand((200 + warmup + steps, n_envs, 4), dtype=torch.float64, device=dev,
+    acts_m = lo + (hi - lo) * torch.rand((pre_steps + warmup + steps, n_envs, 4), dtype=torch.float64, device=dev,
                                          generator=g)
-    for t in range(200):  # mid-episode, as the headline window
+    for t in range(pre_steps):  # the headline's window (--pre-steps untimed env-steps since reset)
         bm.step(acts_m[t])
     tc0 = bm.tier_counts()
-    it = iter(acts_m[200:])
+    it = iter(acts_m[pre_steps:])
     val = timed(lambda: bm.step(next(it)))
     tc = [x - y for x, y in zip(bm.tier_counts(), tc0)]
     tot = float(n_envs * (warmup + steps))
     out["main_mesh_gym_v2"] = {"value": val, "unit": "env-steps/s", "envs": n_envs, "substeps_per_env_step": 2,
+                               "pre_steps_untimed": pre_steps,
                                "model": MODEL_VARIANT["main_mesh"],
                                "kernel_resources": bm.kernel_info(),
                                "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
@@ -652,7 +653,7 @@ def main():
         extra = None
         if world == 1 and not args.no_extra and args.model == "main":
             try:
-                extra = other_configs(n_envs=n)
+                extra = other_configs(n_envs=n, pre_steps=args.pre_steps)
             except Exception as e:  # secondary numbers never fail the headline line
                 extra = {"error": repr(e)}
         line = {
