@@ -1,7 +1,7 @@
 """Long GPU-vs-oracle rollout (checker, test infrastructure): N gym ur3e-v2 envs x S env-steps of
 uniform random actions, crossing the T = 2500 truncation (auto-resets) and every contact / fallback
 transition that occurs; compares every obs/reward/done each step and the full state at the end.
-usage: python tools/long_parity.py [n_envs] [steps]   (prints one JSON line)"""
+usage: python tools/long_parity.py [n_envs] [steps] [model: main | main_mesh]   (prints one JSON line)"""
 import json
 import os
 import sys
@@ -13,11 +13,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def main(n=4096, steps=3000, seed=21):
+def main(n=4096, steps=3000, model="main", seed=21):
     import torch
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
-    md, mc = rt.load_model("main")
+    md, mc = rt.load_model(model)
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=seed)
     gb = rt.Batch(mc, cfg, n)
     ob = po.OracleBatch(mc, po.config_from(cfg), n)
@@ -42,7 +42,7 @@ def main(n=4096, steps=3000, seed=21):
     qp, qv, _ = gb.get_state()
     oqp, oqv, _, onc = ob.get_state()
     ncon = gb.get_info()["ncon"].cpu().numpy()
-    print(json.dumps(dict(envs=n, steps=steps, every_step_bit_exact=first_bad is None, first_mismatch_step=first_bad,
+    print(json.dumps(dict(model=model, envs=n, steps=steps, every_step_bit_exact=first_bad is None, first_mismatch_step=first_bad,
                           episodes_ended=dones, fallback_env_steps=int(gb.overflow_count() - ovf0),
                           max_abs_qpos=float(np.abs(qp.cpu().numpy() - oqp).max()),
                           max_abs_qvel=float(np.abs(qv.cpu().numpy() - oqv).max()),
@@ -51,4 +51,4 @@ def main(n=4096, steps=3000, seed=21):
 
 
 if __name__ == "__main__":
-    main(*[int(x) for x in sys.argv[1:3]])
+    main(*[int(x) for x in sys.argv[1:3]], *sys.argv[3:4])

@@ -2,7 +2,7 @@
 along build_traj_l_pick_place rows through the grasp and lift, where envs hold 12-20 contacts and
 the library routes them to the grasp tier (and switches the pre-pass on and off as the host sees
 routing); compares the full state every `every` rows and at the end, and reports the tier counts.
-usage: python tools/long_parity_c3.py [n_envs] [rows] [every]   (prints one JSON line per check)"""
+usage: python tools/long_parity_c3.py [n_envs] [rows] [every] [model: main | main_mesh]   (prints one JSON line per check)"""
 import json
 import os
 import sys
@@ -14,11 +14,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def main(n=1024, rows=3000, every=250):
+def main(n=1024, rows=3000, every=250, model="main"):
     import torch
     from oracle import pyoracle as po
     from ur3e_amd.controller.move_l_mug import MoveLMug
-    drv = MoveLMug(n, reset_mode="low", seed=7)
+    drv = MoveLMug(n, reset_mode="low", seed=7, model=model)
     gb = drv.batch
     ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n)
     t0 = time.time()
@@ -43,9 +43,9 @@ def main(n=1024, rows=3000, every=250):
         print(json.dumps({"row": t + 1, "max_abs_state_diff": d, "ncon_mismatch": int((ncon != onc).sum()),
                           "ncon_max": int(ncon.max()), "tiers": list(gb.tier_counts()),
                           "elapsed_s": round(time.time() - t0, 1)}), flush=True)
-    print(json.dumps({"envs": n, "rows": rows, "bit_exact": worst == 0.0}), flush=True)
+    print(json.dumps({"model": model, "envs": n, "rows": rows, "bit_exact": worst == 0.0}), flush=True)
     drv.close()
 
 
 if __name__ == "__main__":
-    main(*[int(x) for x in sys.argv[1:4]])
+    main(*[int(x) for x in sys.argv[1:4]], *sys.argv[4:5])
