@@ -410,6 +410,13 @@ struct KState {
 /* host-side routing decision (ur3e_batch_step): run-ahead bound and how long routing stays on after
    the host last saw a routed env */
 #define W_AHEAD 16
+/* the run-ahead event is recorded every W_AHEAD_EVERY steps (a marker on the stream costs ~2-5 us of GPU
+   time per record, profiles/r05_l): step k (k a multiple of it) waits for the marker of step k - W_AHEAD */
+#ifndef W_AHEAD_EVERY
+#define W_AHEAD_EVERY 8
+#endif
+static_assert(W_AHEAD % W_AHEAD_EVERY == 0, "run-ahead bound: a whole number of marker intervals");
+#define W_AHEAD_NEV (W_AHEAD / W_AHEAD_EVERY + 1) /* marker ring: the waited slot is never the one re-recorded */
 #define W_NTOTAL 5 /* device counters of ur3e_batch::d_ovf_total */
 #define W_ROUTE_HOLD 64
 
@@ -1997,9 +2004,10 @@ struct ur3e_batch {
   int* d_pred_ctl;
   hipStream_t side; /* the grasp-tier pre-pass runs here, concurrently with the compact tier */
   hipEvent_t ev_fork, ev_join;
-  /* bounded run-ahead (grasp tier on): step k waits for step k - W_AHEAD to finish before it enqueues,
-     so the host-mapped routed count it reads is at most W_AHEAD steps old */
-  hipEvent_t ev_ahead[16];
+  /* bounded run-ahead (grasp tier on): step k (a multiple of W_AHEAD_EVERY) waits for step k - W_AHEAD to
+     finish before it enqueues, so the host-mapped routed count it reads is at most W_AHEAD + W_AHEAD_EVERY
+     steps old */
+  hipEvent_t ev_ahead[W_AHEAD_NEV];
   long long hstep;      /* steps enqueued outside graph capture */
   long long last_route; /* hstep at which the host last saw a nonzero routed count */
   int queued;      /* compact tier through the substep work queue (w_env_step_q) */
@@ -2290,7 +2298,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
-    for (int k = 0; k < 16; k++) HIPCHK(hipEventCreateWithFlags(&b->ev_ahead[k], hipEventDisableTiming));
+    for (int k = 0; k < W_AHEAD_NEV; k++) HIPCHK(hipEventCreateWithFlags(&b->ev_ahead[k], hipEventDisableTiming));
   }
   /* substep work queue: gym tasks with several substeps per env-step on main.xml's compact tier
      (cfg->schedule 1 keeps one workgroup per env-step) */
@@ -2367,7 +2375,7 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
     (void)hipStreamDestroy(b->side);
     (void)hipEventDestroy(b->ev_fork);
     (void)hipEventDestroy(b->ev_join);
-    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev_ahead[k]);
+    for (int k = 0; k < W_AHEAD_NEV; k++) (void)hipEventDestroy(b->ev_ahead[k]);
   }
   if (b->d_flags) (void)hipFree(b->d_flags);
   if (b->d_mid) (void)hipFree(b->d_mid);
@@ -2529,8 +2537,8 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
       HIPCHK(hipStreamIsCapturing(st, &cs));
       capturing = cs != hipStreamCaptureStatusNone;
       if (!capturing) {
-        const int slot = (int)(b->hstep % W_AHEAD);
-        if (b->hstep >= W_AHEAD) HIPCHK(hipEventSynchronize(b->ev_ahead[slot]));
+        if (b->hstep >= W_AHEAD && b->hstep % W_AHEAD_EVERY == 0)
+          HIPCHK(hipEventSynchronize(b->ev_ahead[((b->hstep - W_AHEAD) / W_AHEAD_EVERY) % W_AHEAD_NEV]));
         if (*(volatile int*)b->h_routed > 0) b->last_route = b->hstep;
       }
       /* routing stays on for W_ROUTE_HOLD steps after the last sighting (it comes in bursts: grasps) */
@@ -2559,7 +2567,7 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
                        d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs);
   HIPCHK(hipGetLastError());
   if (b->tiered && b->grasp && !capturing) {
-    HIPCHK(hipEventRecord(b->ev_ahead[b->hstep % W_AHEAD], st));
+    if (b->hstep % W_AHEAD_EVERY == 0) HIPCHK(hipEventRecord(b->ev_ahead[(b->hstep / W_AHEAD_EVERY) % W_AHEAD_NEV], st));
     b->hstep++;
   }
   if (record) {
