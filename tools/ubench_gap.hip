@@ -8,10 +8,12 @@
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 
+struct BigArg { double v[112]; };  /* a ~900 B by-value argument, like the queue kernel's KConfig + KState */
+
 template <int WR>
-__global__ void __launch_bounds__(64, 2) k_long(double* out, double* big, int iters) {
+__global__ void __launch_bounds__(64, 2) k_long(double* out, double* big, int iters, BigArg ba) {
   extern __shared__ double lds[];
-  double x = threadIdx.x * 1e-3 + blockIdx.x;
+  double x = threadIdx.x * 1e-3 + blockIdx.x + ba.v[(blockIdx.x & 7) * 13] + ba.v[111]; /* uniform reads */
   for (int i = 0; i < iters; i++) x = x * 0.999999 + 1e-9;
   lds[threadIdx.x] = x;
   __builtin_amdgcn_wave_barrier();
@@ -51,11 +53,13 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const int iters = 20000, reps = 200;
+  BigArg ba;
+  for (int k = 0; k < 112; k++) ba.v[k] = 0.0;
   auto launch_long = [&](int wr) {
-    if (wr == 0) hipLaunchKernelGGL(k_long<0>, dim3(2048), dim3(64), 16384, s, d, big, iters);
-    if (wr == 1) hipLaunchKernelGGL(k_long<1>, dim3(2048), dim3(64), 16384, s, d, big, iters);
-    if (wr == 2) hipLaunchKernelGGL(k_long<2>, dim3(2048), dim3(64), 16384, s, d, big, iters);
-    if (wr == 3) hipLaunchKernelGGL(k_long<3>, dim3(2048), dim3(64), 16384, s, d, big, iters);
+    if (wr == 0) hipLaunchKernelGGL(k_long<0>, dim3(2048), dim3(64), 16384, s, d, big, iters, ba);
+    if (wr == 1) hipLaunchKernelGGL(k_long<1>, dim3(2048), dim3(64), 16384, s, d, big, iters, ba);
+    if (wr == 2) hipLaunchKernelGGL(k_long<2>, dim3(2048), dim3(64), 16384, s, d, big, iters, ba);
+    if (wr == 3) hipLaunchKernelGGL(k_long<3>, dim3(2048), dim3(64), 16384, s, d, big, iters, ba);
   };
   hipEvent_t evn[16];
   for (int k = 0; k < 16; k++) hipEventCreateWithFlags(&evn[k], hipEventDisableTiming);
