@@ -2124,6 +2124,58 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
   }
   pl->nfixgrp = ng;
   pl->nfixrow = nr;
+  /* constraint sources (KPlan.cs_*): the row groups' constants with their index chains resolved; the sums
+     are the device's own additions in its order, so the values are bit-identical */
+  auto cs_sol = [&](int r, const double* ref, const double* imp) {
+    for (int k = 0; k < 2; k++) pl->cs_d[r][k] = ref[k];
+    for (int k = 0; k < 5; k++) pl->cs_d[r][2 + k] = imp[k];
+  };
+  for (int e = 0; e < m->neq; e++) {
+    cs_sol(e, m->eq_solref[e], m->eq_solimp[e]);
+    if (m->eq_type[e] == UR3E_EQ_CONNECT) {
+      const int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      pl->cs_i[e][0] = m->body_rootid[b1]; pl->cs_i[e][1] = m->body_rootid[b2];
+      pl->cs_i[e][2] = (int)pl->body_dof_mask[b1]; pl->cs_i[e][3] = (int)pl->body_dof_mask[b2];
+      pl->cs_d[e][7] = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    } else {
+      const int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
+      const int d1 = m->jnt_dofadr[j1], a1 = m->jnt_qposadr[j1];
+      pl->cs_i[e][0] = d1; pl->cs_i[e][2] = a1;
+      pl->cs_d[e][9] = m->qpos0[a1];
+      double diag = m->dof_invweight0[d1];
+      if (j2 >= 0) {
+        const int d2 = m->jnt_dofadr[j2], a2 = m->jnt_qposadr[j2];
+        pl->cs_i[e][1] = d2; pl->cs_i[e][3] = a2;
+        pl->cs_d[e][10] = m->qpos0[a2];
+        diag += m->dof_invweight0[d2];
+      } else {
+        pl->cs_i[e][1] = -1; pl->cs_i[e][3] = 0;
+      }
+      pl->cs_d[e][7] = diag;
+    }
+  }
+  for (int v = 0; v < m->nv; v++) {
+    const int r = W_CS_DOF + v;
+    cs_sol(r, m->dof_solref[v], m->dof_solimp[v]);
+    pl->cs_d[r][7] = m->dof_invweight0[v];
+  }
+  for (int j = 0; j < m->njnt; j++) {
+    const int r = W_CS_JNT + j;
+    cs_sol(r, m->jnt_solref[j], m->jnt_solimp[j]);
+    pl->cs_i[r][0] = m->jnt_dofadr[j]; pl->cs_i[r][2] = m->jnt_qposadr[j];
+    pl->cs_d[r][7] = m->dof_invweight0[m->jnt_dofadr[j]];
+    pl->cs_d[r][8] = m->jnt_margin[j];
+    pl->cs_d[r][9] = m->jnt_range[j][0]; pl->cs_d[r][10] = m->jnt_range[j][1];
+  }
+  for (int p = 0; p < m->ncpair; p++) {
+    const int r = W_CS_PAIR + p;
+    const int b1 = m->geom_bodyid[m->cpair_geom1[p]], b2 = m->geom_bodyid[m->cpair_geom2[p]];
+    cs_sol(r, m->cpair_solref[p], m->cpair_solimp[p]);
+    pl->cs_i[r][0] = m->body_rootid[b1]; pl->cs_i[r][1] = m->body_rootid[b2];
+    pl->cs_i[r][2] = (int)pl->body_dof_mask[b1]; pl->cs_i[r][3] = (int)pl->body_dof_mask[b2];
+    pl->cs_d[r][7] = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    pl->cs_d[r][8] = m->cpair_margin[p] - m->cpair_gap[p];
+  }
 }
 
 extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t* cfg, int n_envs, int device,

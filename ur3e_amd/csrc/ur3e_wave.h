@@ -43,6 +43,11 @@
 /* stage-timing marks of the -DUR3E_STAGE_TIMING build (tools/stage_timing.py) */
 #define W_NSTAGE_MARKS 50
 
+#define W_CS_DOF UR3E_MAXEQ
+#define W_CS_JNT (UR3E_MAXEQ + K_NV)
+#define W_CS_PAIR (UR3E_MAXEQ + K_NV + K_NJ)
+#define W_NCS (W_CS_PAIR + UR3E_MAXCPAIR)
+
 struct KPlan {
   int nlevel;
   int body_depth[K_NB];
@@ -67,6 +72,16 @@ struct KPlan {
   int bj_type[K_NB], bj_qadr[K_NB];
   double bj_q0[K_NB], bj_axis[K_NB][3], bj_pos[K_NB][3];
   int jnt_root[K_NJ];
+  /* constraint sources of the compact tier's row groups (r_mc_rows), one row per source -- equality e,
+     frictionloss dof W_CS_DOF + v, joint limit W_CS_JNT + j, contact pair W_CS_PAIR + p -- with every
+     index chain of the group data resolved on the host, so a group loads its constants one level deep:
+       cs_i: connect / contact: body roots 1, 2 and body dof masks 1, 2; joint equality: dof 1, dof 2
+             (-1: none), qpos address 1, 2; limit: dof, -, qpos address, -;
+       cs_d: solref[2], solimp[5], diag (the sum of the two invweights where there are two, in the
+             device's order), margin (contact: margin - gap), qpos0 at address 1 | range low,
+             qpos0 at address 2 | range high */
+  int cs_i[W_NCS][4];
+  double cs_d[W_NCS][11];
 };
 
 /* constraint row groups (one lane builds one group) */

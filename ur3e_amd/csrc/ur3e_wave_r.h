@@ -1699,6 +1699,11 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
       path per group type (uniform) -> J columns;
    3. lane = row: fetch its group's inputs by lane shuffle, then one common impedance path.
    Same expressions as w_make_constraint's phases A and B. */
+/* the row groups' constants from the host-resolved plan rows (1, default) or through the model's index
+   chains (0: A/B) */
+#ifndef W_FLAT_GROUPS
+#define W_FLAT_GROUPS 1
+#endif
 template <class KS>
 WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
@@ -1709,6 +1714,77 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   double o1[3] = {0, 0, 0}, o2[3] = {0, 0, 0}, fr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   double gpos[3] = {0, 0, 0}, gmargin = 0, gdiag = 0, dpoly = 0, side = 0;
   double sref[2] = {0, 0}, simp[5] = {0, 0, 0, 0, 0};
+#if W_FLAT_GROUPS
+  if (lane < ngrp) {
+    gtype = s.grp_type[lane];
+    const int id = s.grp_id[lane];
+    grow = s.grp_row[lane];
+    /* the group's constants from its plan row (KPlan.cs_*), all loads one level deep and issued before
+       the per-kind branches, which then read only LDS; same values as the index chains below */
+    const int src = gtype <= G_JOINTEQ ? id
+                    : gtype == G_FLOSS ? W_CS_DOF + id
+                    : gtype == G_LIMIT ? W_CS_JNT + (id >> 1)
+                                       : W_CS_PAIR + s.con_cpair[id];
+    int ci[4];
+    double cd[11];
+#pragma unroll
+    for (int k = 0; k < 4; k++) ci[k] = pl->cs_i[src][k];
+#pragma unroll
+    for (int k = 0; k < 11; k++) cd[k] = pl->cs_d[src][k];
+    for (int k = 0; k < 2; k++) sref[k] = cd[k];
+    for (int k = 0; k < 5; k++) simp[k] = cd[2 + k];
+    gdiag = cd[7];
+    if (gtype == G_CONNECT) {
+      const int e = id;
+      double p1[3], p2[3];
+      for (int k = 0; k < 3; k++) { p1[k] = s.eq_p[e][k]; p2[k] = s.eq_p[e][3 + k]; }
+      const int r1 = ci[0], r2 = ci[1];
+      for (int k = 0; k < 3; k++) {
+        o1[k] = p1[k] - s.subtree_com[r1][k];
+        o2[k] = p2[k] - s.subtree_com[r2][k];
+        gpos[k] = p1[k] - p2[k];
+      }
+      msk1 = ci[2]; msk2 = ci[3];
+    } else if (gtype == G_JOINTEQ) {
+      const double* c = m->eq_data[id];
+      dof1 = ci[0];
+      const double q1 = s.qpos[ci[2]] - cd[9];
+      if (ci[1] >= 0) {
+        dof2 = ci[1];
+        const double q2 = s.qpos[ci[3]] - cd[10];
+        dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
+        gpos[0] = q1 - (c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4]))));
+      } else {
+        gpos[0] = q1 - c[0];
+      }
+    } else if (gtype == G_FLOSS) {
+      dof1 = id;
+      fric = 1;
+    } else if (gtype == G_LIMIT) {
+      const int sd = (id & 1) ? 1 : -1;
+      side = (double)sd;
+      dof1 = ci[0];
+      const double q = s.qpos[ci[2]];
+      gpos[0] = sd * ((sd > 0 ? cd[10] : cd[9]) - q);
+      gmargin = cd[8];
+    } else {
+      const int c = id;
+      const int r1 = ci[0], r2 = ci[1];
+      for (int k = 0; k < 3; k++) {
+        const double pk = s.con_pos[c][k];
+        o1[k] = pk - s.subtree_com[r1][k];
+        o2[k] = pk - s.subtree_com[r2][k];
+      }
+      for (int k = 0; k < 3; k++) fr[k] = s.con_n[c][k];
+      k_frame_rest(fr); /* k_make_frame's rows 1-2 from the stored unit normal */
+      msk1 = ci[2]; msk2 = ci[3];
+      const double d = s.con_dist[c];
+      gpos[0] = d; gpos[1] = d; gpos[2] = d;
+      gmargin = cd[8];
+      fric = 2; /* rows k > 0 */
+    }
+  }
+#else
   if (lane < ngrp) {
     gtype = s.grp_type[lane];
     const int id = s.grp_id[lane];
@@ -1788,6 +1864,7 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
       for (int k = 0; k < 5; k++) simp[k] = m->cpair_solimp[p][k];
     }
   }
+#endif
   WT(37);
   /* ---- 2. Jacobian: GS groups side by side per pass (lanes [K_NV t, K_NV t + K_NV) take group
      g0 + t, lane = dof within), the group's data by lane shuffle from its group lane, gathered
