@@ -657,16 +657,22 @@ WD void w_make_carry(KModel m, const KPlan* __restrict__ pl, const KS& s, double
   }
 }
 
+/* mj_objectVelocity of a site (world frame, [w, v]); b, root: the site's body and its root (KPlan.sv_*
+   resolves them on the host for the epilogue's two sites) */
 template <class KS>
-KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
-  int b = m->site_bodyid[site];
+KD void w_site_velocity(KModel m, const KS& s, int site, double res[6], int b, int root) {
   const double* cv = s.cvel[b];
-  const double* c = s.subtree_com[m->body_rootid[b]];
+  const double* c = s.subtree_com[root];
   double dif[3] = {s.site_xpos[site][0] - c[0], s.site_xpos[site][1] - c[1], s.site_xpos[site][2] - c[2]};
   double cr[3];
   k_cross3(cr, dif, cv);
   res[0] = cv[0]; res[1] = cv[1]; res[2] = cv[2];
   res[3] = cv[3] - cr[0]; res[4] = cv[4] - cr[1]; res[5] = cv[5] - cr[2];
+}
+template <class KS>
+KD void w_site_velocity(KModel m, const KS& s, int site, double res[6]) {
+  const int b = m->site_bodyid[site];
+  w_site_velocity(m, s, site, res, b, m->body_rootid[b]);
 }
 
 /* UR3eEnv2._get_obs (ur3e_env2.py:111-123), lane 0.  pads >= 0: the pad-contact scan below done
@@ -2175,6 +2181,18 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     pl->cs_i[r][2] = (int)pl->body_dof_mask[b1]; pl->cs_i[r][3] = (int)pl->body_dof_mask[b2];
     pl->cs_d[r][7] = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
     pl->cs_d[r][8] = m->cpair_margin[p] - m->cpair_gap[p];
+  }
+  for (int p = 0; p < m->ncpair; p++) {
+    const int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
+    pl->pr_i[p][0] = g1; pl->pr_i[p][1] = g2; pl->pr_i[p][2] = m->geom_type[g1]; pl->pr_i[p][3] = m->geom_type[g2];
+    pl->pr_d[p][0] = m->cpair_margin[p];
+    pl->pr_d[p][1] = m->geom_rbound[g1]; pl->pr_d[p][2] = m->geom_rbound[g2];
+    for (int k = 0; k < 3; k++) { pl->pr_d[p][3 + k] = m->geom_size[g1][k]; pl->pr_d[p][6 + k] = m->geom_size[g2][k]; }
+  }
+  const int vsite[2] = {m->id_site_tcp, m->id_site_handle};
+  for (int k = 0; k < 2; k++) {
+    pl->sv_body[k] = vsite[k] >= 0 ? m->site_bodyid[vsite[k]] : -1;
+    pl->sv_root[k] = vsite[k] >= 0 ? m->body_rootid[pl->sv_body[k]] : -1;
   }
 }
 

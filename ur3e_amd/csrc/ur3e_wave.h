@@ -82,6 +82,13 @@ struct KPlan {
              qpos0 at address 2 | range high */
   int cs_i[W_NCS][4];
   double cs_d[W_NCS][11];
+  /* collision candidates (the overlaid layouts' broadphase and narrowphase), one row per pair with its
+     geoms' constants: pr_i = geom 1, geom 2, type 1, type 2; pr_d = margin, rbound 1, rbound 2, size 1[3],
+     size 2[3] */
+  int pr_i[UR3E_MAXCPAIR][4];
+  double pr_d[UR3E_MAXCPAIR][9];
+  /* the epilogue's velocity sites (tcp, handle): body and its root (-1: no such site) */
+  int sv_body[2], sv_root[2];
 };
 
 /* constraint row groups (one lane builds one group) */
@@ -831,12 +838,44 @@ WD void w_solve_tree(KModel m, const KPlan* __restrict__ pl, const double (*A)[K
 /* ================================================================== */
 /* collision: per-candidate lanes, prefix offsets, deterministic order */
 /* ================================================================== */
+/* a candidate pair's constants: from the plan's pair rows (one load level, the overlaid layouts) or
+   through the model's pair -> geom chain (the full-capacity layouts); the same values either way */
+struct WPairRow {
+  int g1, g2, t1, t2;
+  double margin, rb1, rb2;
+  const double* s1; /* the geoms' sizes, in memory: the narrowphase indexes them at run time */
+  const double* s2;
+};
+/* the overlaid box layouts read the plan rows (1, default) or the model's chains (0: A/B) */
+#ifndef W_FLAT_PAIRS
+#define W_FLAT_PAIRS 1
+#endif
+WD WPairRow w_pair_row_m(KModel m, int p) {
+  WPairRow P;
+  P.g1 = m->cpair_geom1[p]; P.g2 = m->cpair_geom2[p];
+  P.t1 = m->geom_type[P.g1]; P.t2 = m->geom_type[P.g2];
+  P.margin = m->cpair_margin[p];
+  P.rb1 = m->geom_rbound[P.g1]; P.rb2 = m->geom_rbound[P.g2];
+  P.s1 = m->geom_size[P.g1]; P.s2 = m->geom_size[P.g2];
+  return P;
+}
+template <class KS>
+WD WPairRow w_pair_row(KModel m, const KPlan* __restrict__ pl, int p) {
+  /* the mesh-capable layouts keep the model's chains: measured 0.3 % slower with the rows (A/B 5) */
+  if (!W_FLAT_PAIRS || KS::MESHES) return w_pair_row_m(m, p);
+  WPairRow P;
+  P.g1 = pl->pr_i[p][0]; P.g2 = pl->pr_i[p][1]; P.t1 = pl->pr_i[p][2]; P.t2 = pl->pr_i[p][3];
+  P.margin = pl->pr_d[p][0]; P.rb1 = pl->pr_d[p][1]; P.rb2 = pl->pr_d[p][2];
+  P.s1 = &pl->pr_d[p][3]; P.s2 = &pl->pr_d[p][6];
+  return P;
+}
+
 /* bounding-sphere test of candidate pair p (mj_collideGeoms' rbound early-out) */
 template <class KS>
-WD bool w_pair_near(KModel m, const KS& s, int p) {
-  int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
-  double margin = m->cpair_margin[p];
-  double rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
+WD bool w_pair_near(const KS& s, const WPairRow& P) {
+  const int g1 = P.g1, g2 = P.g2;
+  const double margin = P.margin;
+  const double rb1 = P.rb1, rb2 = P.rb2;
   if (rb1 > 0 && rb2 > 0) {
     double dx = s.geom_xpos[g1][0] - s.geom_xpos[g2][0];
     double dy = s.geom_xpos[g1][1] - s.geom_xpos[g2][1];
@@ -857,10 +896,10 @@ WD bool w_pair_near(KModel m, const KS& s, int p) {
    the hull's bounding radius; box-mesh and mesh-mesh: the hulls' boxes (below).  Either way
    the pair's result (no contact) is unchanged, and only its narrowphase is skipped. */
 template <class KS>
-WD bool w_pair_apart(KModel m, const KS& s, int p) {
-  const int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
-  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const double margin = m->cpair_margin[p];
+WD bool w_pair_apart(const KS& s, const WPairRow& P) {
+  const int g1 = P.g1, g2 = P.g2;
+  const int t1 = P.t1, t2 = P.t2;
+  const double margin = P.margin;
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_MESH) {
     /* every hull vertex lies within geom_rbound of the geom's origin (the compiler's bound over the
        same vertices), so the centre beyond the margin by more than rbound + 1e-9 keeps every vertex
@@ -869,7 +908,7 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
     const double n[3] = {pm[2], pm[5], pm[8]};
     const double dif[3] = {s.geom_xpos[g2][0] - s.geom_xpos[g1][0], s.geom_xpos[g2][1] - s.geom_xpos[g1][1],
                            s.geom_xpos[g2][2] - s.geom_xpos[g1][2]};
-    return k_dot3(n, dif) - m->geom_rbound[g2] > margin + 1e-9;
+    return k_dot3(n, dif) - P.rb2 > margin + 1e-9;
   }
   const bool mesh2 = t2 == UR3E_GEOM_MESH, mesh1 = t1 == UR3E_GEOM_MESH;
   if (t2 != UR3E_GEOM_BOX && !mesh2) return false;
@@ -883,7 +922,7 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
     const double dist = k_dot3(n, dif);
     double ext = 0;
 #pragma unroll
-    for (int c = 0; c < 3; c++) ext += m->geom_size[g2][c] * fabs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]);
+    for (int c = 0; c < 3; c++) ext += P.s2[c] * fabs(n[0] * bm[c] + n[1] * bm[3 + c] + n[2] * bm[6 + c]);
     return dist - ext > margin + 1e-9;
   }
   if (t1 != UR3E_GEOM_BOX && !mesh1) return false;
@@ -894,8 +933,8 @@ WD bool w_pair_apart(KModel m, const KS& s, int p) {
   const double lim = (mesh1 || mesh2) ? margin + 1e-6 : margin;
   const double* R1 = s.geom_xmat[g1];
   const double* R2 = s.geom_xmat[g2];
-  const double* s1 = m->geom_size[g1];
-  const double* s2 = m->geom_size[g2];
+  const double* s1 = P.s1;
+  const double* s2 = P.s2;
   double a[3][3], b[3][3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -1011,10 +1050,10 @@ struct KStageEmit {
 
 /* w_narrow_core with the compact tier's LDS clip buffers and contact stage (lane ln < W_NP_LANES) */
 template <class KS>
-WD int w_narrow_lds(KModel m, KS& s, int p, int ln, int slot) {
-  int g1 = m->cpair_geom1[p], g2 = m->cpair_geom2[p];
-  double margin = m->cpair_margin[p];
-  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+WD int w_narrow_lds(KS& s, const WPairRow& P, int ln, int slot) {
+  const int g1 = P.g1, g2 = P.g2;
+  const double margin = P.margin;
+  const int t1 = P.t1, t2 = P.t2;
   auto& ch = s.kn.chunk();
   const KStageEmit<KS::NPST> emit{&ch.np_stage[0][0], ch.np_key, &ch.np_nstage, ln};
   /* convex meshes: the mesh-capable layouts settle a pair whose hulls are apart beyond the margin (GJK,
@@ -1037,19 +1076,18 @@ WD int w_narrow_lds(KModel m, KS& s, int p, int ln, int slot) {
     }
   }
   if (t1 == UR3E_GEOM_PLANE && t2 == UR3E_GEOM_BOX)
-    return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], m->geom_size[g2],
-                         margin, emit);
+    return k_plane_box_t(s.geom_xpos[g1], s.geom_xmat[g1], s.geom_xpos[g2], s.geom_xmat[g2], P.s2, margin, emit);
   if (t1 == UR3E_GEOM_BOX && t2 == UR3E_GEOM_BOX) {
     KLdsClip clip{&ch.np_clip[0][0][0][0], ln};
-    return k_box_box_t(s.geom_xpos[g1], s.geom_xmat[g1], m->geom_size[g1], s.geom_xpos[g2], s.geom_xmat[g2],
-                       m->geom_size[g2], margin, clip, emit);
+    return k_box_box_t(s.geom_xpos[g1], s.geom_xmat[g1], P.s1, s.geom_xpos[g2], s.geom_xmat[g2], P.s2, margin, clip,
+                       emit);
   }
   return 0;
 }
 
 template <class KS>
 WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
-  return w_pair_near(m, s, p) ? w_narrow_core(m, s, p, raw) : 0;
+  return w_pair_near(s, w_pair_row_m(m, p)) ? w_narrow_core(m, s, p, raw) : 0;
 }
 
 /* mesh-capable overlaid layouts: every survivor pair with a convex mesh (plane-mesh, box-mesh, mesh-mesh)
@@ -1057,7 +1095,7 @@ WD int w_narrow(KModel m, const KS& s, int p, KRaw* raw) {
    bit for bit); its raw contacts wait in s.kn.mres until the chunked narrowphase emits them at the pair's
    place.  More raw contacts than the layout holds, or an EPA horizon beyond WC_MAXE, hand the env-step on. */
 template <class KS>
-WD void w_mesh_pass(KModel m, KS& s, int nsurv) {
+WD void w_mesh_pass(KModel m, const KPlan* __restrict__ pl, KS& s, int nsurv) {
   const int lane = w_lane();
   auto& R = s.kn.mres;
   auto& W = s.kn.cw;
@@ -1153,7 +1191,7 @@ __device__ __forceinline__ int* w_near_list(KS& s) {
 #define W_BROAD_2PASS 1
 #endif
 template <class KS>
-WD void r_collision(KModel m, KS& s) {
+WD void r_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
   const int np = m->ncpair;
   int nsurv = 0;
@@ -1170,7 +1208,7 @@ WD void r_collision(KModel m, KS& s) {
     int nnear = 0;
     for (int base = 0; base < np; base += 64) {
       const int p = base + lane;
-      const bool ok = p < np && w_pair_near(m, s, p);
+      const bool ok = p < np && w_pair_near(s, w_pair_row<KS>(m, pl, p));
       const unsigned long long bm = __ballot(ok);
       const int at = nnear + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
       if (ok && at < NCAP) near[at] = p;
@@ -1182,7 +1220,7 @@ WD void r_collision(KModel m, KS& s) {
     for (int base = 0; base < nnear; base += 64) {
       const int k = base + lane;
       const int p = k < nnear ? near[k] : 0;
-      const bool ok = k < nnear && !w_pair_apart(m, s, p);
+      const bool ok = k < nnear && !w_pair_apart(s, w_pair_row<KS>(m, pl, p));
       const unsigned long long bm = __ballot(ok);
       const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
       if (ok && at < CAP) s.cand_off[at] = p;
@@ -1191,7 +1229,11 @@ WD void r_collision(KModel m, KS& s) {
   } else {
     for (int base = 0; base < np; base += 64) {
       const int p = base + lane;
-      const bool ok = p < np && w_pair_near(m, s, p) && !(W_PAIR_CULL && w_pair_apart(m, s, p));
+      bool ok = false;
+      if (p < np) {
+        const WPairRow P = w_pair_row<KS>(m, pl, p);
+        ok = w_pair_near(s, P) && !(W_PAIR_CULL && w_pair_apart(s, P));
+      }
       const unsigned long long bm = __ballot(ok);
       const int at = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
       if (ok && at < CAP) s.cand_off[at] = p;
@@ -1215,7 +1257,7 @@ WD void r_collision(KModel m, KS& s) {
     constexpr int NST = KS::NPST;
     static_assert(KS::BAIL && KS::MAXCON <= NST && NST <= 64, "compact narrowphase stage must hold MAXCON");
     if constexpr (KS::MESHES) {
-      w_mesh_pass(m, s, nsurv);
+      w_mesh_pass(m, pl, s, nsurv);
       WT(48);
     }
     auto& ch = s.kn.chunk();
@@ -1228,7 +1270,7 @@ WD void r_collision(KModel m, KS& s) {
       const bool act = lane < npl && slot < nsurv;
       const int p = s.cand_off[act ? slot : 0];
       int cnt = 0;
-      if (act) cnt = w_narrow_lds(m, s, p, lane, slot);
+      if (act) cnt = w_narrow_lds(s, w_pair_row<KS>(m, pl, p), lane, slot);
       int incl = cnt;
 #pragma unroll
       for (int d = 1; d < W_NP_LANES; d <<= 1) {
@@ -1328,9 +1370,9 @@ WD void w_collision_all(KModel m, KS& s) {
 }
 
 template <int NT, class KS>
-WD void w_collision(KModel m, KS& s) {
+WD void w_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if constexpr (NT == 64) {
-    r_collision<KS>(m, s);
+    r_collision<KS>(m, pl, s);
   } else {
     w_collision_all<NT>(m, s);
   }
@@ -2352,14 +2394,17 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0, b
     if (tid < 2) {
       const int site = tid == 0 ? m->id_site_tcp : m->id_site_handle;
       double v[6] = {0, 0, 0, 0, 0, 0};
-      if (site >= 0) w_site_velocity(m, s, site, v);
+      if (site >= 0) {
+        if (W_FLAT_PAIRS) w_site_velocity(m, s, site, v, pl->sv_body[tid], pl->sv_root[tid]);
+        else w_site_velocity(m, s, site, v);
+      }
       for (int k = 0; k < 6; k++) s.site_vel[tid][k] = v[k];
     }
     WT(6);
     W_DBL(7, w_rne_passive<NT>(m, pl, s));
     WT(7);
   }
-  W_DBL(4, w_collision<NT>(m, s));
+  W_DBL(4, w_collision<NT>(m, pl, s));
   WT(4);
   if (KS::BAIL && s.ovf) return;
   W_DBL(5, w_make_constraint<NT>(m, pl, s));
