@@ -2189,6 +2189,31 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     pl->pr_d[p][1] = m->geom_rbound[g1]; pl->pr_d[p][2] = m->geom_rbound[g2];
     for (int k = 0; k < 3; k++) { pl->pr_d[p][3 + k] = m->geom_size[g1][k]; pl->pr_d[p][6 + k] = m->geom_size[g2][k]; }
   }
+  for (int v = 0; v < m->nv; v++) {
+    const int j = m->dof_jntid[v];
+    const bool spring = m->jnt_stiffness[j] != 0 &&
+                        (m->jnt_type[j] == UR3E_JNT_HINGE || m->jnt_type[j] == UR3E_JNT_SLIDE) && m->jnt_dofadr[j] == v;
+    pl->pd_i[v][0] = m->dof_bodyid[v];
+    pl->pd_i[v][1] = spring ? m->jnt_qposadr[j] : 0;
+    pl->pd_d[v][0] = spring ? m->jnt_stiffness[j] : 0.0;
+    pl->pd_d[v][1] = spring ? m->qpos_spring[m->jnt_qposadr[j]] : 0.0;
+    pl->pd_d[v][2] = m->dof_damping[v];
+  }
+  for (int a = 0; a < m->nu; a++) {
+    pl->pa_i[a][0] = m->act_ctrllimited[a] ? 1 : 0;
+    pl->pa_i[a][1] = m->act_biastype[a] == UR3E_BIAS_AFFINE ? 1 : 0;
+    pl->pa_i[a][2] = m->act_forcelimited[a] ? 1 : 0;
+    pl->pa_i[a][3] = m->act_trntype[a] == UR3E_TRN_JOINT ? m->jnt_qposadr[m->act_trnid[a]] : -1;
+    pl->pa_d[a][0] = m->act_ctrlrange[a][0]; pl->pa_d[a][1] = m->act_ctrlrange[a][1];
+    pl->pa_d[a][2] = m->act_gainprm[a][0];
+    for (int k = 0; k < 3; k++) pl->pa_d[a][3 + k] = m->act_biasprm[a][k];
+    pl->pa_d[a][6] = m->act_forcerange[a][0]; pl->pa_d[a][7] = m->act_forcerange[a][1];
+    pl->pa_d[a][8] = m->act_gear[a];
+  }
+  for (int e = 0; e < m->neq; e++) {
+    pl->eqc_i[e][0] = m->eq_type[e] == UR3E_EQ_CONNECT ? 1 : 0;
+    pl->eqc_i[e][1] = m->eq_obj1[e]; pl->eqc_i[e][2] = m->eq_obj2[e];
+  }
   const int vsite[2] = {m->id_site_tcp, m->id_site_handle};
   for (int k = 0; k < 2; k++) {
     pl->sv_body[k] = vsite[k] >= 0 ? m->site_bodyid[vsite[k]] : -1;

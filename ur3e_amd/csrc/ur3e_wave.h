@@ -89,7 +89,22 @@ struct KPlan {
   double pr_d[UR3E_MAXCPAIR][9];
   /* the epilogue's velocity sites (tcp, handle): body and its root (-1: no such site) */
   int sv_body[2], sv_root[2];
+  /* per dof, the passive forces' constants: pd_i = body, spring qpos address; pd_d = stiffness where
+     the dof's joint has a spring term (hinge or slide, its first dof; else 0), qpos_spring there, damping */
+  int pd_i[K_NV][2];
+  double pd_d[K_NV][3];
+  /* per actuator: pa_i = ctrllimited, affine bias, forcelimited, qpos address of a joint transmission
+     (-1: tendon); pa_d = ctrlrange[2], gainprm[0], biasprm[0..2], forcerange[2], gear */
+  int pa_i[K_NU][4];
+  double pa_d[K_NU][9];
+  /* per equality: connect (1 / 0), body 1, body 2 */
+  int eqc_i[UR3E_MAXEQ][3];
 };
+/* the per-dof / per-actuator / per-equality plan rows of com_pos and the passive and actuator forces
+   (1, default) or the model's index chains (0: A/B) */
+#ifndef W_FLAT_DYN
+#define W_FLAT_DYN 1
+#endif
 
 /* constraint row groups (one lane builds one group) */
 #define G_CONNECT 0
@@ -660,8 +675,10 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
   if constexpr (KS::OVERLAY) {
     /* connect anchors for the constraint rows (r_mc_rows), while xmat is still alive */
     for (int e = tid; e < m->neq; e += NT) {
-      if (m->eq_type[e] != UR3E_EQ_CONNECT) continue;
-      const int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+      int isc, b1, b2;
+      if (W_FLAT_DYN) { isc = pl->eqc_i[e][0]; b1 = pl->eqc_i[e][1]; b2 = pl->eqc_i[e][2]; }
+      else { isc = m->eq_type[e] == UR3E_EQ_CONNECT; b1 = m->eq_obj1[e]; b2 = m->eq_obj2[e]; }
+      if (!isc) continue;
       double p1[3], p2[3];
       k_mat_vec3(p1, s.xmat[b1], m->eq_data[e]);
       p1[0] += s.xpos[b1][0]; p1[1] += s.xpos[b1][1]; p1[2] += s.xpos[b1][2];
@@ -705,9 +722,12 @@ WD void w_com_pos(KModel m, const KPlan* __restrict__ pl, KS& s) {
     }
   }
   for (int a = tid; a < m->nu; a += NT) {
-    double g = m->act_gear[a];
-    if (m->act_trntype[a] == UR3E_TRN_JOINT) {
-      s.actuator_length[a] = s.qpos[m->jnt_qposadr[m->act_trnid[a]]] * g;
+    double g;
+    int qa;
+    if (W_FLAT_DYN) { g = pl->pa_d[a][8]; qa = pl->pa_i[a][3]; }
+    else { g = m->act_gear[a]; qa = m->act_trntype[a] == UR3E_TRN_JOINT ? m->jnt_qposadr[m->act_trnid[a]] : -1; }
+    if (qa >= 0) {
+      s.actuator_length[a] = s.qpos[qa] * g;
     } else {
       int t = m->act_trnid[a];
       double len = 0;
@@ -1696,6 +1716,39 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
   }
   SYNC();
   }
+  if constexpr (W_FLAT_DYN) {
+    /* the same terms from the plan's per-dof and per-actuator rows (one load level) */
+    if (tid < nv) {
+      const int v = tid;
+      const int bv = pl->pd_i[v][0], qa = pl->pd_i[v][1];
+      const double k = pl->pd_d[v][0], spring = pl->pd_d[v][1], b = pl->pd_d[v][2];
+      s.qfrc_bias[v] = k_dot6(s.cdof[v], cfrc[bv]);
+      double pf = 0;
+      if (k != 0) pf = -k * (s.qpos[qa] - spring);
+      if (b != 0) pf -= b * s.qvel[v];
+      s.qfrc_passive[v] = pf;
+    }
+    for (int a = tid; a < m->nu; a += NT) {
+      int ai[4];
+      double ad[9];
+      for (int q = 0; q < 4; q++) ai[q] = pl->pa_i[a][q];
+      for (int q = 0; q < 8; q++) ad[q] = pl->pa_d[a][q];
+      double vel = 0;
+      for (int v = 0; v < nv; v++) vel += pl->act_moment[a][v] * s.qvel[v];
+      double ctrl = s.ctrl[a];
+      if (ai[0]) {
+        if (ctrl < ad[0]) ctrl = ad[0];
+        if (ctrl > ad[1]) ctrl = ad[1];
+      }
+      double f = ad[2] * ctrl;
+      if (ai[1]) f += ad[3] + ad[4] * s.actuator_length[a] + ad[5] * vel;
+      if (ai[2]) {
+        if (f < ad[6]) f = ad[6];
+        if (f > ad[7]) f = ad[7];
+      }
+      s.act_force[a] = f;
+    }
+  } else {
   if (tid < nv) {
     int v = tid;
     s.qfrc_bias[v] = k_dot6(s.cdof[v], cfrc[m->dof_bodyid[v]]);
@@ -1727,6 +1780,7 @@ WD void w_rne_passive(KModel m, const KPlan* __restrict__ pl, KS& s) {
       if (f > m->act_forcerange[a][1]) f = m->act_forcerange[a][1];
     }
     s.act_force[a] = f;
+  }
   }
   SYNC();
   if (tid < nv) {
