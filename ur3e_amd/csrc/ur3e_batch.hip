@@ -2169,6 +2169,7 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     const int r = W_CS_JNT + j;
     cs_sol(r, m->jnt_solref[j], m->jnt_solimp[j]);
     pl->cs_i[r][0] = m->jnt_dofadr[j]; pl->cs_i[r][2] = m->jnt_qposadr[j];
+    pl->cs_i[r][1] = m->jnt_limited[j] && (m->jnt_type[j] == UR3E_JNT_HINGE || m->jnt_type[j] == UR3E_JNT_SLIDE);
     pl->cs_d[r][7] = m->dof_invweight0[m->jnt_dofadr[j]];
     pl->cs_d[r][8] = m->jnt_margin[j];
     pl->cs_d[r][9] = m->jnt_range[j][0]; pl->cs_d[r][10] = m->jnt_range[j][1];
@@ -2213,6 +2214,13 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
   for (int e = 0; e < m->neq; e++) {
     pl->eqc_i[e][0] = m->eq_type[e] == UR3E_EQ_CONNECT ? 1 : 0;
     pl->eqc_i[e][1] = m->eq_obj1[e]; pl->eqc_i[e][2] = m->eq_obj2[e];
+  }
+  for (int f = 0; f < m->ngeom + m->nsite; f++) {
+    const bool geom = f < m->ngeom;
+    const int q = geom ? f : f - m->ngeom;
+    pl->fr_b[f] = geom ? m->geom_bodyid[q] : m->site_bodyid[q];
+    for (int c = 0; c < 3; c++) pl->fr_d[f][c] = geom ? m->geom_pos[q][c] : m->site_pos[q][c];
+    for (int c = 0; c < 4; c++) pl->fr_d[f][3 + c] = geom ? m->geom_quat[q][c] : m->site_quat[q][c];
   }
   const int vsite[2] = {m->id_site_tcp, m->id_site_handle};
   for (int k = 0; k < 2; k++) {

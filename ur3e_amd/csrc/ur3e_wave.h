@@ -76,7 +76,7 @@ struct KPlan {
      frictionloss dof W_CS_DOF + v, joint limit W_CS_JNT + j, contact pair W_CS_PAIR + p -- with every
      index chain of the group data resolved on the host, so a group loads its constants one level deep:
        cs_i: connect / contact: body roots 1, 2 and body dof masks 1, 2; joint equality: dof 1, dof 2
-             (-1: none), qpos address 1, 2; limit: dof, -, qpos address, -;
+             (-1: none), qpos address 1, 2; limit: dof, limited hinge / slide (1 / 0), qpos address, -;
        cs_d: solref[2], solimp[5], diag (the sum of the two invweights where there are two, in the
              device's order), margin (contact: margin - gap), qpos0 at address 1 | range low,
              qpos0 at address 2 | range high */
@@ -99,6 +99,9 @@ struct KPlan {
   double pa_d[K_NU][9];
   /* per equality: connect (1 / 0), body 1, body 2 */
   int eqc_i[UR3E_MAXEQ][3];
+  /* the kinematics' frames, geoms then sites: body, pos[3], quat[4] */
+  int fr_b[UR3E_MAXGEOM + UR3E_MAXSITE];
+  double fr_d[UR3E_MAXGEOM + UR3E_MAXSITE][7];
 };
 /* the per-dof / per-actuator / per-equality plan rows of com_pos and the passive and actuator forces
    (1, default) or the model's index chains (0: A/B) */

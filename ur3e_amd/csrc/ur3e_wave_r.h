@@ -1276,7 +1276,14 @@ WD void r_kinematics(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int ng = m->ngeom, nfr = m->ngeom + m->nsite;
   int fb = 0;
   double fpos[3] = {0, 0, 0}, fquat[4] = {1, 0, 0, 0};
-  if (lane < ng) {
+  if (W_FLAT_DYN) {
+    /* geoms then sites, one plan row each (KPlan.fr_*): one branch and one load level */
+    if (lane < nfr) {
+      fb = pl->fr_b[lane];
+      for (int c = 0; c < 3; c++) fpos[c] = pl->fr_d[lane][c];
+      for (int c = 0; c < 4; c++) fquat[c] = pl->fr_d[lane][3 + c];
+    }
+  } else if (lane < ng) {
     fb = m->geom_bodyid[lane];
     for (int c = 0; c < 3; c++) fpos[c] = m->geom_pos[lane][c];
     for (int c = 0; c < 4; c++) fquat[c] = m->geom_quat[lane][c];
@@ -1637,11 +1644,32 @@ WD void r_cfrc(KModel m, KS& s) {
    joint limits in (joint, side) order; condim-3 contacts in contact order) by ballot prefix
    sums instead of a serial lane-0 walk.  Any layout that would not fit the compact capacity
    bails (ovf): the full-capacity tier then reproduces the oracle's truncation rule. */
+/* the row groups' constants from the host-resolved plan rows (1, default) or through the model's index
+   chains (0: A/B) */
+#ifndef W_FLAT_GROUPS
+#define W_FLAT_GROUPS 1
+#endif
 template <class KS>
 WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
   const int nj = m->njnt, ncon = s.ncon;
   int lo = 0, hi = 0;
+#if W_FLAT_GROUPS
+  /* the joint's limit row of the plan (limited hinge / slide flag, qpos address, margin, range): one load
+     level, issued before the test */
+  if (lane < nj) {
+    const int r = W_CS_JNT + lane;
+    const int lim = pl->cs_i[r][1], qa = pl->cs_i[r][2];
+    const double mg = pl->cs_d[r][8], rlo = pl->cs_d[r][9], rhi = pl->cs_d[r][10];
+    if (lim) {
+      const double q = s.qpos[qa];
+      const double dlo = -1.0 * (rlo - q);
+      const double dhi = 1.0 * (rhi - q);
+      lo = dlo < mg;
+      hi = dhi < mg;
+    }
+  }
+#else
   if (lane < nj && m->jnt_limited[lane] &&
       (m->jnt_type[lane] == UR3E_JNT_HINGE || m->jnt_type[lane] == UR3E_JNT_SLIDE)) {
     const double q = s.qpos[m->jnt_qposadr[lane]];
@@ -1651,6 +1679,7 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
     lo = dlo < mg;
     hi = dhi < mg;
   }
+#endif
   int c3 = 0;
   if (lane < ncon) c3 = m->cpair_condim[s.con_cpair[lane]] == 3;
   const unsigned long long mlo = __ballot(lo), mhi = __ballot(hi), mc = __ballot(c3);
@@ -1699,11 +1728,6 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
       path per group type (uniform) -> J columns;
    3. lane = row: fetch its group's inputs by lane shuffle, then one common impedance path.
    Same expressions as w_make_constraint's phases A and B. */
-/* the row groups' constants from the host-resolved plan rows (1, default) or through the model's index
-   chains (0: A/B) */
-#ifndef W_FLAT_GROUPS
-#define W_FLAT_GROUPS 1
-#endif
 template <class KS>
 WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
