@@ -48,6 +48,12 @@ struct RRow {
   int st, flag;
 };
 
+/* the packed-triangle hand-offs without per-element branches (1, default; see the stores) or with them
+   (0: A/B) */
+#ifndef W_HL_ORDERED
+#define W_HL_ORDERED 1
+#endif
+
 /* value of a per-row quantity at row `src` (any slot): a lane shuffle of the slot that holds it.
    With one slot this is the plain shuffle (src 64, 65 wrap to lanes 0, 1 as before; never used). */
 template <int RPL>
@@ -559,7 +565,14 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   /* block-diagonal: the cross block is the oracle's exact +0 (not stored) */
   const int cfrom = bd && row >= SPLIT ? SPLIT : 0;
 #pragma unroll
+#if W_HL_ORDERED
+  for (int c = 0; c < K_NV; c++) { /* unconditional reads, as in the tree factorisation */
+    const double v = s.Hl[KTRI(row, c)];
+    h[c] = (c <= row && c >= cfrom) ? v : 0.0;
+  }
+#else
   for (int c = 0; c < K_NV; c++) h[c] = (c <= row && c >= cfrom) ? s.Hl[KTRI(row, c)] : 0.0;
+#endif
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   WT(10);
@@ -641,9 +654,21 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   /* L^T via LDS (packed lower triangle; the Cholesky's column slots are done with, and nothing else
      reads it during the solves); the diagonal comes back on its own lane */
   if (lane < nv) {
+#if W_HL_ORDERED
+    /* every lane writes its whole row, c descending, with no per-element branch: a write past the
+       diagonal (c > lane) lands on an element (L2, c2) of a later row L2 > lane with c2 < c, which lane
+       L2 writes in a later instruction, so the valid value wins (one wave's LDS writes complete in
+       order; the compiler barriers keep the program order) */
+#pragma unroll
+    for (int c = K_NV - 1; c >= 0; c--) {
+      s.Hl[KTRI(lane, c)] = h[c];
+      asm volatile("" ::: "memory");
+    }
+#else
 #pragma unroll
     for (int c = 0; c < K_NV; c++)
       if (c <= lane) s.Hl[KTRI(lane, c)] = h[c];
+#endif
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
@@ -1156,16 +1181,35 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   if (lane < nv) x *= dinv;
   /* column -> row hand-off through the packed lower triangle (ancestors have lower indices) */
   if (lane < nv) {
+#if W_HL_ORDERED
+    /* every lane writes its whole column, i ascending, with no per-element branch: a write above the
+       diagonal (i < lane) lands on an element (i2, c2) of a later row i2 > i, written in a later
+       instruction, so the valid value wins (as in the Newton direction's L' hand-off) */
+#pragma unroll
+    for (int i = 0; i < K_NV; i++) {
+      s.Hl[KTRI(i, lane)] = a[i];
+      asm volatile("" ::: "memory");
+    }
+#else
 #pragma unroll
     for (int i = 0; i < K_NV; i++)
       if (i >= lane) s.Hl[KTRI(i, lane)] = a[i];
+#endif
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   const unsigned int myam = lane < nv ? pl->dof_anc_mask[lane] : 0u;
   double r[K_NV];
 #pragma unroll
+#if W_HL_ORDERED
+  /* unconditional reads (KTRI(col, j) < K_NV (K_NV + 1) / 2 for every j): no per-element branch */
+  for (int j = 0; j < K_NV; j++) {
+    const double v = s.Hl[KTRI(col, j)];
+    r[j] = j <= col ? v : 0.0;
+  }
+#else
   for (int j = 0; j < K_NV; j++) r[j] = j <= col ? s.Hl[KTRI(col, j)] : 0.0;
+#endif
   if constexpr (SPLIT > 0) {
     /* paired again: ancestor j of a lane is in the lane's own tree, ascending within it */
     constexpr int NVS = KS::NV;
