@@ -2222,6 +2222,26 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
     for (int c = 0; c < 3; c++) pl->fr_d[f][c] = geom ? m->geom_pos[q][c] : m->site_pos[q][c];
     for (int c = 0; c < 4; c++) pl->fr_d[f][3 + c] = geom ? m->geom_quat[q][c] : m->site_quat[q][c];
   }
+  /* the Newton direction's element slots (r_direction's mapping, dense and block-diagonal) */
+  for (int bdm = 0; bdm < 2; bdm++) {
+    const int nv = m->nv, S = bdm ? UR3E_MAIN_SPLIT : 0;
+    const bool bd = S > 0;
+    const int nel = nv * (nv + 1) / 2, nel1 = S * (S + 1) / 2;
+    const int nelb = bd ? nel1 + (nv - S) * (nv - S + 1) / 2 : nel;
+    for (int lane = 0; lane < 64; lane++)
+      for (int q = 0; q < W_HB_NQ; q++) {
+        const int e = lane + 64 * q;
+        const bool ev = e < nelb;
+        const bool b2 = bd && e >= nel1;
+        const int t = ev ? (b2 ? e - nel1 : e) : 0;
+        int a = 0;
+        while ((a + 1) * (a + 2) / 2 <= t) a++;
+        const int off = b2 ? S : 0;
+        const int k = off + a, c = off + t - a * (a + 1) / 2;
+        const int ek = ev ? k : 0, ec = ev ? c : 0, ep = ev ? KTRI(k, c) : 0;
+        pl->hb_map[bdm][lane][q] = ek | (ec << 8) | (ep << 16) | ((ev ? 1 : 0) << 24);
+      }
+  }
   const int vsite[2] = {m->id_site_tcp, m->id_site_handle};
   for (int k = 0; k < 2; k++) {
     pl->sv_body[k] = vsite[k] >= 0 ? m->site_bodyid[vsite[k]] : -1;

@@ -43,6 +43,11 @@
 /* stage-timing marks of the -DUR3E_STAGE_TIMING build (tools/stage_timing.py) */
 #define W_NSTAGE_MARKS 50
 
+#define W_HB_NQ ((K_NV * (K_NV + 1) / 2 + 63) / 64)
+/* the Newton direction's element slots from the plan (1, default) or solved per call (0: A/B) */
+#ifndef W_HB_MAP
+#define W_HB_MAP 1
+#endif
 #define W_CS_DOF UR3E_MAXEQ
 #define W_CS_JNT (UR3E_MAXEQ + K_NV)
 #define W_CS_PAIR (UR3E_MAXEQ + K_NV + K_NJ)
@@ -102,6 +107,10 @@ struct KPlan {
   /* the kinematics' frames, geoms then sites: body, pos[3], quat[4] */
   int fr_b[UR3E_MAXGEOM + UR3E_MAXSITE];
   double fr_d[UR3E_MAXGEOM + UR3E_MAXSITE][7];
+  /* the Newton direction's element slots (r_direction): lane l, slot q holds lower-triangle element
+     (k, c) at packed index p, for the dense [0] and the block-diagonal [1] Hessian (UR3E_MAIN_SPLIT):
+     k | c << 8 | p << 16 | valid << 24 */
+  int hb_map[2][64][W_HB_NQ];
 };
 /* the per-dof / per-actuator / per-equality plan rows of com_pos and the passive and actuator forces
    (1, default) or the model's index chains (0: A/B) */
@@ -2487,7 +2496,7 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0, b
   }
 solve:
   if constexpr (REG)
-    W_DBL(15, r_solve_newton(m, s));
+    W_DBL(15, r_solve_newton(m, pl, s));
   else
     w_solve_newton<NT>(m, s);
   WT(15);

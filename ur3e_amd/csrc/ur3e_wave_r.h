@@ -375,7 +375,7 @@ struct RIc {
 /* Newton direction: H = M + J'DJ + cone terms (lane k = row k), Cholesky in registers,
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
 template <class KS>
-WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
+WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow (&W)[KS::RPL], double grad) {
   constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
@@ -454,6 +454,23 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
   int ek[NQ], ec[NQ], ep[NQ];
   bool ev[NQ];
   double hv[NQ];
+#if W_HB_MAP
+  static_assert(NQ <= W_HB_NQ, "H element map: more slots than the plan holds");
+  {
+    /* the lane's element slots from the plan (KPlan.hb_map, the same mapping computed on the host for
+       both cases of the block-diagonal flag): one load instead of the triangle-row solve per slot */
+    const int* hm = pl->hb_map[(SPLIT > 0 && bd) ? 1 : 0][lane];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int w = hm[q];
+      ev[q] = (w >> 24) & 1;
+      ek[q] = w & 0xff;
+      ec[q] = (w >> 8) & 0xff;
+      ep[q] = (w >> 16) & 0xff;
+      hv[q] = s.qMp[ep[q]];
+    }
+  }
+#else
 #pragma unroll
   for (int q = 0; q < NQ; q++) {
     const int e = lane + 64 * q;
@@ -469,6 +486,7 @@ WD double r_direction(KModel m, KS& s, const RRow (&W)[KS::RPL], double grad) {
     ep[q] = ev[q] ? KTRI(k, c) : 0; /* packed index of element (ek, ec) */
     hv[q] = s.qMp[ep[q]];
   }
+#endif
   /* only rows that add to H are visited, in row order (the others add nothing in the oracle):
      quadratic rows and the first row of each cone-state contact; slot h covers rows 64h..
      Rows go in chunks of CH.  Every row's increment is independent of hv: D jk jc for a quadratic
@@ -962,7 +980,7 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
 #define RDBL(k, stmt) do { stmt; if (UR3E_DOUBLE_STAGE == (k)) { stmt; } } while (0)
 /* w_solve_newton for the compact tier; leaves s.qacc and s.qfrc_constraint */
 template <class KS>
-WD void r_solve_newton(KModel m, KS& s) {
+WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
   constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m);
@@ -1007,7 +1025,7 @@ WD void r_solve_newton(KModel m, KS& s) {
   RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
   WT(9);
   double search;
-  RDBL(20, search = r_direction(m, s, W, grad));
+  RDBL(20, search = r_direction(m, pl, s, W, grad));
   WT(11);
   for (int iter = 0; iter < m->iterations; iter++) {
     double alpha;
@@ -1029,7 +1047,7 @@ WD void r_solve_newton(KModel m, KS& s) {
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
-    RDBL(20, search = r_direction(m, s, W, grad));
+    RDBL(20, search = r_direction(m, pl, s, W, grad));
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
