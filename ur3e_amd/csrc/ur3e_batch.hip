@@ -2238,7 +2238,9 @@ static void build_plan(const ur3e_model_t* m, KPlan* pl) {
         while ((a + 1) * (a + 2) / 2 <= t) a++;
         const int off = b2 ? S : 0;
         const int k = off + a, c = off + t - a * (a + 1) / 2;
-        const int ek = ev ? k : 0, ec = ev ? c : 0, ep = ev ? KTRI(k, c) : 0;
+        /* an invalid slot aliases the lane's slot 0 element (r_direction stores slot 0 last) */
+        const int ep0 = q > 0 ? (pl->hb_map[bdm][lane][0] >> 16) & 0xff : 0;
+        const int ek = ev ? k : 0, ec = ev ? c : 0, ep = ev ? KTRI(k, c) : ep0;
         pl->hb_map[bdm][lane][q] = ek | (ec << 8) | (ep << 16) | ((ev ? 1 : 0) << 24);
       }
   }

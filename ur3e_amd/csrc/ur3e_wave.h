@@ -109,7 +109,7 @@ struct KPlan {
   double fr_d[UR3E_MAXGEOM + UR3E_MAXSITE][7];
   /* the Newton direction's element slots (r_direction): lane l, slot q holds lower-triangle element
      (k, c) at packed index p, for the dense [0] and the block-diagonal [1] Hessian (UR3E_MAIN_SPLIT):
-     k | c << 8 | p << 16 | valid << 24 */
+     k | c << 8 | p << 16 | valid << 24; an invalid slot's p is the lane's slot-0 element */
   int hb_map[2][64][W_HB_NQ];
 };
 /* the per-dof / per-actuator / per-equality plan rows of com_pos and the passive and actuator forces

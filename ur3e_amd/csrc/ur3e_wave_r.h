@@ -574,9 +574,21 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
     hbuild(RIc<NQ>{});
   }
   /* element slot q of this lane is packed-triangle index ep[q] */
+#if W_HB_MAP
+  if (nelb >= 64) {
+    /* every lane's slot 0 is valid and the plan aliases its invalid slots to slot 0's element
+       (KPlan.hb_map), so the slots are stored without a per-lane condition, slot 0 last: its valid
+       value overwrites the alias (same lane, program order) */
 #pragma unroll
-  for (int q = 0; q < NQ; q++)
-    if (q < nqe && ev[q]) s.Hl[ep[q]] = hv[q];
+    for (int q = NQ - 1; q >= 0; q--)
+      if (q < nqe) s.Hl[ep[q]] = hv[q];
+  } else
+#endif
+  {
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      if (q < nqe && ev[q]) s.Hl[ep[q]] = hv[q];
+  }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   double h[K_NV];
