@@ -387,6 +387,22 @@ __device__ __forceinline__ double qm_get(const KS& s, int i, int j) {
   if constexpr (KS::OVERLAY) return s.qMp[i >= j ? KTRI(i, j) : KTRI(j, i)];
   else return s.qM[i][j];
 }
+/* the overlaid layouts' packed mass-matrix element (row, j) for loops over a compile-time j: the byte
+   offset is a per-row base plus a constant either side of the diagonal (rb + 8 j for j <= row, by symmetry
+   8 row + 8 KTRI(j, 0) for j > row), and the right one is always the larger (T(row) + j >= T(j) + row
+   exactly when j <= row, T(n) = n (n + 1) / 2; equal offsets are the same element): two adds and a max per
+   element instead of the max / min / multiply of KTRI(max, min), and no per-element compare mask; the same
+   element as qm_get(s, row, j) */
+struct QmIx {
+  int rb, rc, row;
+};
+__device__ __forceinline__ QmIx qm_ix(int row) { return QmIx{8 * KTRI(row, 0), 8 * row, row}; }
+template <class KS>
+__device__ __forceinline__ double qm_at(const KS& s, const QmIx& q, int j) {
+  const int a = q.rb + 8 * j, b = q.rc + 8 * KTRI(j, 0);
+  const int off = a > b ? a : b;
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(s.qMp) + off);
+}
 /* full-capacity tier: the oracle's limits (UR3E_MAXCON contacts, UR3E_MAXEFC rows) */
 typedef KSX<K_MAXCON, K_MAXEFC> KSL;
 /* compact tier: sized for the gym workload on main.xml -- the mug resting on the table (4 contacts,

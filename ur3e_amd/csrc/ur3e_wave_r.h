@@ -48,6 +48,10 @@ struct RRow {
   int st, flag;
 };
 
+/* the packed mass matrix read with per-row byte bases (1, default) or by KTRI(max, min) (0: A/B) */
+#ifndef W_QM_IX
+#define W_QM_IX 1
+#endif
 /* the packed-triangle hand-offs without per-element branches (1, default; see the stores) or with them
    (0: A/B) */
 #ifndef W_HL_ORDERED
@@ -281,9 +285,10 @@ WD void r_eval_state(KModel m, KS& s, RRow (&W)[KS::RPL], double qacc, double qs
   {
     double v = 0;
     const int row = lane < nv ? lane : 0;
+    const QmIx qi = qm_ix(row);
 #pragma unroll
     for (int j = 0; j < K_NV; j++)
-      if (j < nv) v += qm_get(s, row, j) * qv[j];
+      if (j < nv) v += (W_QM_IX ? qm_at(s, qi, j) : qm_get(s, row, j)) * qv[j];
     Ma = v;
   }
 #pragma unroll
@@ -925,9 +930,10 @@ WD double r_line_search(KModel m, KS& s, RRow (&W)[KS::RPL], double search, doub
   {
     double v = 0;
     const int row = lane < nv ? lane : 0;
+    const QmIx qi = qm_ix(row);
 #pragma unroll
     for (int j = 0; j < K_NV; j++)
-      if (j < nv) v += qm_get(s, row, j) * sv[j];
+      if (j < nv) v += (W_QM_IX ? qm_at(s, qi, j) : qm_get(s, row, j)) * sv[j];
     Mv = v;
   }
 #pragma unroll
@@ -1087,8 +1093,11 @@ WD double r_tree_solve(KModel m, const KPlan* __restrict__ pl, KS& s, bool dampe
   for (int k = 0; k < K_NV; k++)
     amask[k] = KS::STATIC_TREE ? (k < UR3E_MAIN_NV ? ur3e_main_dof_anc_mask[k] : 0u) : pl->dof_anc_mask[k];
   double a[K_NV];
+  {
+    const QmIx qc = qm_ix(col); /* M[i][col] = M[col][i]: the same packed element */
 #pragma unroll
-  for (int i = 0; i < K_NV; i++) a[i] = qm_get(s, i, col);
+    for (int i = 0; i < K_NV; i++) a[i] = W_QM_IX ? qm_at(s, qc, i) : qm_get(s, i, col);
+  }
   if (damped) {
     const double hstep = m->timestep;
     const double dmp = lane < nv ? m->dof_damping[col] : 0.0;
