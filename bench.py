@@ -5,12 +5,20 @@ mug, contacts on), gymnasium `ur3e-v2` step semantics (pid_task_ctrl + 2
 physics substeps + obs/reward/termination + auto-reset at T=2500), uniformly
 random task-space actions in the v2 action Box, 4096 envs per GPU.  One
 "step" = one env-step of all resident envs = one ur3e_batch_step call: the
-compact-tier kernel w_env_step<64, KSS_NV> (one wavefront per env, working set
-in LDS) plus the full-capacity fallback kernel over the envs it queued.
+compact-tier kernel (w_env_step_q: a substep work queue, one wavefront per
+env-substep, working set in LDS) plus the full-capacity fallback kernel over
+the envs it queued.
 
-Multi-GPU: one process per GPU (torchrun), envs sharded by contiguous global
-id (weak scaling: 4096 per GPU), per-step RCCL gather of (obs, reward, done)
-to rank 0 (the policy rank) as the north_star's C4 prescribes.
+Multi-GPU: one process per GPU, envs sharded by contiguous global id (weak
+scaling: 4096 per GPU), per-step RCCL gather of (obs, reward, done) to rank 0
+(the policy rank) as the north_star's C4 prescribes.  Under torchrun the ranks
+come from its environment; `python bench.py --gpus N` without it starts the N
+rank processes itself (`launch_workers`, before this process touches a GPU)
+and fails when fewer than N GPUs are visible.
+
+Model: `--model main_mesh` (the default) is main.xml with convex hulls for its
+mesh geoms -- the reference's collision set (24 geoms, 234 candidate pairs);
+`--model main` is the box surrogate, measured beside it in `other_configs`.
 
 Prints ONE JSON line on rank 0 (see the contract in the task statement).
 """
@@ -36,11 +44,88 @@ FP64_VECTOR_PEAK_TFLOPS = 78.6
 
 
 # the two compiles of the reference's assets/main.xml (ur3e_amd/model/compiler.py): its mesh files are
-# git-ignored upstream, so the headline runs the documented box surrogate; main_mesh has SURVEY §2.3's collision
-# set with synthetic convex stand-in hulls for every mesh file (tools/make_main_meshes.py)
+# git-ignored upstream: main_mesh (the headline) has SURVEY §2.3's collision set, with synthetic convex stand-in
+# hulls for every mesh file (tools/make_main_meshes.py); main is the documented box surrogate
 MODEL_VARIANT = {"main": "model variant: box surrogate for the mesh geoms (15 colliding geoms, 92 candidate pairs)",
                  "main_mesh": "model variant: convex stand-in hulls for the mesh geoms (24 colliding geoms, 17 meshes, "
                               "234 candidate pairs)"}
+
+
+def shard_offset(rank: int, envs_per_gpu: int) -> int:
+    """first global env id of a rank's shard (contiguous ranges, weak scaling)"""
+    return rank * envs_per_gpu
+
+
+def launch_mode(gpus: int, environ) -> str:
+    """"rank": this process is one rank of a launched job (WORLD_SIZE set, by torchrun or launch_workers);
+    "spawn": start `gpus` rank processes (launch_workers); "single": one GPU, this process."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if gpus != 1 and int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}")
+        return "rank"
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    return "spawn" if gpus > 1 else "single"
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(n: int, argv, script: str | None = None, check_devices: bool = True, stdout=None,
+                   timeout: float | None = None) -> int:
+    """Start `n` rank processes of `script` (default: this file) with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set, one GPU each, and return the job's exit status (the first non-zero
+    one; the other ranks are then terminated).  This process only counts the devices -- no HIP call --
+    so the ranks start from a GPU-clean parent; more ranks than visible GPUs fail before any start."""
+    import signal
+    import subprocess
+    if check_devices:
+        import torch
+        have = torch.cuda.device_count()  # counts devices without initialising one (no HIP context)
+        if n > have:
+            print(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv),
+                                      env=env, stdout=stdout))
+    t0 = time.monotonic()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                print(f"bench.py: ranks still running after {timeout} s", file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:  # only these exact children
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc < 0:  # a rank died of a signal: report it as the shell would
+        rc = 128 - rc
+    return rc
 
 
 def _profile_file(kind: str):
@@ -125,7 +210,8 @@ def _time_oracle(ob, actions_fn, steps):
 def cpu_other_configs(L, threads, c2_envs=4096, c2_steps=200, c3_envs=1024, c3_rows=(1500, 1800)):
     """Oracle CPU figures for the other single-GPU configs, on `threads` host threads:
     C2 -- ur3e_2f85, random joint targets through move_j's PD (as other_configs);
-    C3 -- main.xml move_l_mug scripted pick, the rows c3_rows of the grasp window (reached untimed)."""
+    C3 -- main.xml move_l_mug scripted pick, the rows c3_rows of the grasp window (reached untimed), on
+    both compiles of main.xml (the box surrogate and the convex hulls)."""
     from oracle import pyoracle as po
     from ur3e_amd import runtime as rt
     from ur3e_amd.controller.move_l_mug import MoveLMug
@@ -146,29 +232,32 @@ def cpu_other_configs(L, threads, c2_envs=4096, c2_steps=200, c3_envs=1024, c3_r
     dt = _time_oracle(ob, act, c2_steps)
     out["C2_ur3e_2f85_move_j"] = {"value": c2_envs * c2_steps / dt, "unit": "env-steps/s", "cores": threads,
                                   "sample": f"{c2_envs} envs x {c2_steps} move_j env-steps, {dt:.1f} s"}
-    drv = MoveLMug(c3_envs, reset_mode="low", seed=0)   # trajectory rows only (evaluated on the GPU)
-    ob = po.OracleBatch(drv.batch.model_c, po.config_from(drv.batch.cfg), c3_envs, L=L)
-    g0, g1 = c3_rows
-    for t in range(g0):
-        ob.step(drv.traj.row(t).cpu().numpy())
-    rows = [drv.traj.row(t).cpu().numpy() for t in range(g0, g1)]
-    dt = _time_oracle(ob, lambda i: rows[i], g1 - g0)
-    drv.close()
-    out["C3_main_move_l_mug"] = {"value": c3_envs * (g1 - g0) / dt, "unit": "env-steps/s", "cores": threads,
-                                 "sample": f"{c3_envs} envs x rows {g0}-{g1} of the scripted pick (grasp window, "
-                                           f"reached untimed), {dt:.1f} s"}
+    for model in ("main", "main_mesh"):
+        drv = MoveLMug(c3_envs, reset_mode="low", seed=0, model=model)  # trajectory rows only (GPU-evaluated)
+        ob = po.OracleBatch(drv.batch.model_c, po.config_from(drv.batch.cfg), c3_envs, L=L)
+        g0, g1 = c3_rows
+        for t in range(g0):
+            ob.step(drv.traj.row(t).cpu().numpy())
+        rows = [drv.traj.row(t).cpu().numpy() for t in range(g0, g1)]
+        dt = _time_oracle(ob, lambda i: rows[i], g1 - g0)
+        drv.close()
+        out[f"C3_{model}_move_l_mug"] = {
+            "value": c3_envs * (g1 - g0) / dt, "unit": "env-steps/s", "cores": threads,
+            "sample": f"{c3_envs} envs x rows {g0}-{g1} of the scripted pick (grasp window, reached untimed), "
+                      f"{dt:.1f} s", "model": MODEL_VARIANT[model]}
     return out
 
 
 def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_core_steps=400,
-                 all_cores_steps=100):
+                 all_cores_steps=100, model="main_mesh"):
     """The cpu_baseline leg.  The oracle (oracle/, the same algorithm in C) is compiled for this host
     (-O3 -march=native -ffp-contract=off, OpenMP over envs) and timed on a bounded sample of the bench
     workload: (1) this process's CPU share (OMP_NUM_THREADS, 16 per GPU on the box): n_envs_sample gym
     ur3e-v2 envs x `steps` env-steps; (2) every core of the affinity mask: n_envs_sample x all_cores_steps;
     (3) one thread: one_core_envs x one_core_steps; (4) C2 and C3 on the CPU share.  As the checker, the
     same seeded actions of (1) are replayed through a fresh GPU handle, giving the metric's second half,
-    max |qpos - ref| after `steps` env-steps (the oracle is the reference here: MuJoCo is absent)."""
+    max |qpos - ref| after `steps` env-steps (the oracle is the reference here: MuJoCo is absent).
+    `model`: the compile of main.xml the headline runs (main_mesh: convex hulls; main: box surrogate)."""
     import tempfile
 
     import torch
@@ -176,7 +265,7 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
     from ur3e_amd import runtime as rt
     L = po.load_native(os.path.join(tempfile.gettempdir(), f"ur3e_oracle_native_{os.getpid()}"))
     threads = _host_threads()
-    md, mc = rt.load_model("main")
+    md, mc = rt.load_model(model)
     c = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, model=md, seed=seed)
     lo = np.array([0.04799994, -0.11650084, 0.0, 0.0])
     hi = np.array([0.54799994, 0.38349916, 0.5, 1.0])
@@ -193,8 +282,8 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         dt += time.perf_counter() - t0
         gb.step(torch.from_numpy(a))
     torch.cuda.synchronize()
-    parity = dict(workload="gym ur3e-v2, uniform random actions", envs=n_envs_sample, steps=steps,
-                  **_state_diff(gb, ob))
+    parity = dict(workload="gym ur3e-v2, uniform random actions", model=MODEL_VARIANT[model], envs=n_envs_sample,
+                  steps=steps, **_state_diff(gb, ob))
     gb.close()
     # (2) one thread
     L.ur3o_set_threads(1)
@@ -215,6 +304,7 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         # than the quota only time-share it (round 4 measured 256 threads 28x slower than 16)
         n_all = max(int(quota), 1)
     all_cores = None
+    capped = isinstance(quota, float) and quota < host["affinity_cpus"]
     if n_all != threads:
         L.ur3o_set_threads(n_all)
         oba = po.OracleBatch(mc, po.config_from(c), n_envs_sample, L=L)
@@ -223,8 +313,9 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
         del oba
         all_cores = {"value": n_envs_sample * all_cores_steps / dta, "unit": "env-steps/s", "cores": n_all,
                      "sample": f"{n_envs_sample} envs x {all_cores_steps} env-steps from reset, OpenMP {n_all} "
-                               f"threads (the affinity mask's CPUs, capped at the cgroup's CPU quota {quota}), "
-                               f"{dta:.1f} s"}
+                               f"threads (the affinity mask's CPUs"
+                               + (f", capped at the cgroup's CPU quota {quota}" if capped else "")
+                               + f"), {dta:.1f} s"}
     L.ur3o_set_threads(threads)
     try:
         others = cpu_other_configs(L, threads)
@@ -233,8 +324,9 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
     cpu = _cpu_model()
     build = "gcc -O3 -march=native -ffp-contract=off -fopenmp (compiled on this host)"
     base = dict(value=n_envs_sample * steps / dt, unit="env-steps/s", cores=threads, kind="port",
-                sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, 2 substeps) from reset, "
-                       f"oracle/ C restatement, OpenMP {threads} threads (this process's CPU share), {dt:.1f} s",
+                sample=f"{n_envs_sample} envs x {steps} gym ur3e-v2 env-steps (main.xml, {MODEL_VARIANT[model]}; "
+                       f"2 substeps) from reset, oracle/ C restatement, OpenMP {threads} threads (this process's "
+                       f"CPU share), {dt:.1f} s",
                 cpu_model=cpu, build=build, host=host,
                 all_cores=all_cores,
                 one_core={"value": one_core_envs * one_core_steps / dt1, "unit": "env-steps/s", "cores": 1,
@@ -243,8 +335,9 @@ def cpu_baseline(n_envs_sample=4096, steps=1000, seed=0, one_core_envs=256, one_
     return base, parity
 
 
-def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500):
+def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500, headline_model="main_mesh"):
     """Throughput of the BASELINE configs other than the headline one, on one GPU (rank 0, N=1):
+    the headline workload on the other compile of main.xml (the box surrogate beside the mesh headline);
     C2 -- ur3e_2f85, random joint targets through move_j's PD (one mj_step per control step);
     C3 -- main.xml move_l_mug scripted pick (pid_task_ctrl along build_traj_l_pick_place rows,
     one mj_step per row).  Timed with HIP events on the library's stream, inputs resident."""
@@ -284,9 +377,10 @@ def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500):
     out["C2_ur3e_2f85_move_j"] = {"value": timed(lambda: b.step(next(it))), "unit": "env-steps/s",
                                   "envs": n_envs, "substeps_per_env_step": 1}
     b.close()
-    # the headline workload on main.xml with convex meshes (synthetic stand-in hulls for the mesh files the
-    # reference does not ship, tools/make_main_meshes.py): the mesh-capable tier set, GJK in the compact tier
-    md_m, mc_m = rt.load_model("main_mesh")
+    # the headline workload on the other compile of main.xml: the box surrogate beside the convex-hull headline
+    # (or the hulls -- the mesh-capable tier set, GJK/EPA in the wavefront -- beside a box-surrogate headline)
+    other = "main" if headline_model == "main_mesh" else "main_mesh"
+    md_m, mc_m = rt.load_model(other)
     cfg_m = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md_m, seed=1234)
     bm = rt.Batch(mc_m, cfg_m, n_envs)
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
@@ -300,9 +394,9 @@ def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500):
     val = timed(lambda: bm.step(next(it)))
     tc = [x - y for x, y in zip(bm.tier_counts(), tc0)]
     tot = float(n_envs * (warmup + steps))
-    out["main_mesh_gym_v2"] = {"value": val, "unit": "env-steps/s", "envs": n_envs, "substeps_per_env_step": 2,
+    out[f"{other}_gym_v2"] = {"value": val, "unit": "env-steps/s", "envs": n_envs, "substeps_per_env_step": 2,
                                "pre_steps_untimed": pre_steps,
-                               "model": MODEL_VARIANT["main_mesh"],
+                               "model": MODEL_VARIANT[other],
                                "kernel_resources": bm.kernel_info(),
                                "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
                                "grasp_tier_routed_frac": tc[2] / tot}
@@ -390,7 +484,7 @@ def c3_mesh(n_envs=4096, rows=(1500, 5000)):
     tot = float(n_envs * (g1 - g0))
     res = {"value": tot / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s", "envs": n_envs,
            "substeps_per_env_step": 1, "rows": [g0, g1], "model": MODEL_VARIANT["main_mesh"],
-           "kernel_resources": drv.batch.kernel_info(),
+           "kernel_resources": drv.batch.kernel_info(), "grasp_kernel_resources": drv.batch.kernel_info("grasp"),
            "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot}
     drv.close()
     return res
@@ -402,7 +496,8 @@ def c5_ppo_rollout(n_envs=4096, n_steps=16, iterations=3):
     (config_rl.yml: n_steps 16, batch 256, 30 epochs, net_arch [256, 256]; VecNormalize(norm_obs, clip 10),
     train_rl.py:57), restated on the device (ur3e_amd/rl/ppo.py: SB3 is not installed): the UR3eVecEnv
     (this library) -> on-device VecNormalize -> the actor-critic's forward, no host round trip.  Reported:
-    the rollout's env-steps/s (env + normalisation + policy), the same env-steps through the env and
+    `value`, BASELINE's C5 metric -- wall-clock env-steps/s of whole PPO iterations (rollout plus update) --;
+    the rollout's env-steps/s alone (env + normalisation + policy), the same env-steps through the env and
     VecNormalize alone with resident actions (the env's share), and the PPO update per iteration."""
     import torch
     from ur3e_amd.envs.vec_env import UR3eVecEnv
@@ -429,8 +524,11 @@ def c5_ppo_rollout(n_envs=4096, n_steps=16, iterations=3):
     env_s = (time.perf_counter() - t0) / iterations
     venv.close()
     k = n_steps * n_envs
-    return {"value": k / roll, "unit": "env-steps/s", "envs": n_envs,
-            "what": "PPO rollout: env + on-device VecNormalize + policy inference ([256, 256] tanh MLP, f32)",
+    return {"value": k / (roll + train), "unit": "env-steps/s", "envs": n_envs,
+            "what": "wall-clock PPO iterations: rollout (env + on-device VecNormalize + policy inference, "
+                    "[256, 256] tanh MLP, f32) plus the PPO update (out of scope: DESIGN.md §8)",
+            "rollout_env_steps_per_s": {"value": k / roll, "unit": "env-steps/s",
+                                        "what": "the rollout alone: env + VecNormalize + policy inference"},
             "env_and_vecnormalize_only": {"value": k / env_s, "unit": "env-steps/s"},
             "policy_share_of_rollout": 1.0 - env_s / roll,
             "rollout_ms_per_env_step": 1e3 * roll / n_steps,
@@ -440,21 +538,22 @@ def c5_ppo_rollout(n_envs=4096, n_steps=16, iterations=3):
                        "source": "ur3e_amd/rl/ppo.py (SB3 PPO restated; SB3 absent)"}}
 
 
-def move_l_mug_parity(n_envs=512, steps=1000, seed=0):
+def move_l_mug_parity(n_envs=512, steps=1000, seed=0, model="main_mesh"):
     """Checker for the north_star's parity clause: the move_l_mug scripted grasp (C3 semantics:
     pid_task_ctrl along per-env build_traj_l_pick_place rows, one mj_step per row, 'low' mug noise)
     for `steps` rows on the GPU and on the oracle; max |qpos - ref| and ncon mismatches at the end."""
     import torch
     from oracle import pyoracle as po
     from ur3e_amd.controller.move_l_mug import MoveLMug
-    drv = MoveLMug(n_envs, reset_mode="low", seed=seed)
+    drv = MoveLMug(n_envs, reset_mode="low", seed=seed, model=model)
     gb = drv.batch
     ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n_envs)
     for _ in range(steps):
         row = drv.step()
         ob.step(row.cpu().numpy())
     torch.cuda.synchronize()
-    out = dict(workload="move_l_mug scripted pick (main.xml, pid_task_ctrl, 1 substep)", envs=n_envs,
+    out = dict(workload="move_l_mug scripted pick (main.xml, pid_task_ctrl, 1 substep)", model=MODEL_VARIANT[model],
+               envs=n_envs,
                steps=steps, **_state_diff(gb, ob))
     drv.close()
     return out
@@ -477,12 +576,17 @@ def main():
                          "(default: the library's)")
     ap.add_argument("--pre-steps", type=int, default=500,
                     help="untimed env-steps after reset, so the timed window is mid-episode (contact regime)")
-    ap.add_argument("--model", default="main", choices=["main", "main_mesh"],
-                    help="main: main.xml's box-surrogate compile (the headline); main_mesh: main.xml with convex "
-                         "stand-in hulls for its mesh files (the reference's collision set)")
+    ap.add_argument("--model", default="main_mesh", choices=["main", "main_mesh"],
+                    help="main_mesh (the headline): main.xml with convex stand-in hulls for its mesh files (the "
+                         "reference's collision set); main: main.xml's box-surrogate compile")
     ap.add_argument("--gather-self", action="store_true",
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
+    ap.add_argument("--launch-timeout", type=float, default=None,
+                    help="--gpus N without torchrun: seconds before the rank processes are stopped")
     args = ap.parse_args()
+    if launch_mode(args.gpus, os.environ) == "spawn":
+        # one process per GPU, started before anything here touches a GPU (this process only counts them)
+        sys.exit(launch_workers(args.gpus, sys.argv[1:], timeout=args.launch_timeout))
 
     import torch
     import torch.distributed as dist
@@ -518,11 +622,15 @@ def main():
     n = args.envs_per_gpu
     md, mc = rt.load_model(args.model)
     cfg = rt.make_config(task=rt.TASK_GYM_V2, frame_skip=2, max_episode_steps=2500, model=md, seed=1234,
-                         env_id_offset=rank * n, envs_per_block=args.envs_per_block)
+                         env_id_offset=shard_offset(rank, n), envs_per_block=args.envs_per_block)
     batch = rt.Batch(mc, cfg, n, device=local)
     if args.queue_split is not None:
         batch.set_queue_split(args.queue_split)
     batch_kinfo = batch.kernel_info()
+    try:
+        full_kinfo = batch.kernel_info("full")
+    except RuntimeError:  # an untiered layout has no fallback tier
+        full_kinfo = {}
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
     gen = torch.Generator(device=dev)
@@ -649,18 +757,19 @@ def main():
             except Exception:
                 fp64 = None
         cpu, parity = None, None
-        if not args.no_cpu_baseline and world == 1 and args.model == "main":
+        if not args.no_cpu_baseline and world == 1:
             try:
-                cpu, p_gym = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
-                parity = {"gym_v2": p_gym, "move_l_mug": move_l_mug_parity(steps=args.cpu_sample_steps),
+                cpu, p_gym = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps, model=args.model)
+                parity = {"gym_v2": p_gym,
+                          "move_l_mug": move_l_mug_parity(steps=args.cpu_sample_steps, model=args.model),
                           "reference": "oracle/ (CPU restatement; MuJoCo 3.3.3 absent: parity vs MuJoCo unpinned)",
                           "tolerance": 1e-5}
             except Exception as e:  # the oracle is only the checker; never fail the bench on it
                 cpu = dict(value=None, unit="env-steps/s", cores=None, kind="port", sample=f"failed: {e}")
         extra = None
-        if world == 1 and not args.no_extra and args.model == "main":
+        if world == 1 and not args.no_extra:
             try:
-                extra = other_configs(n_envs=n, pre_steps=args.pre_steps)
+                extra = other_configs(n_envs=n, pre_steps=args.pre_steps, headline_model=args.model)
             except Exception as e:  # secondary numbers never fail the headline line
                 extra = {"error": repr(e)}
         line = {
@@ -686,6 +795,7 @@ def main():
                                             -64: "full-capacity, 64 lanes per env"}.get(
                            batch.cfg.envs_per_block, f"v1 lane-per-env, {batch.cfg.envs_per_block} envs/wave"),
                        "kernel_resources": batch_kinfo,
+                       "fallback_kernel_resources": full_kinfo,
                        "queue_split_percent": args.queue_split if args.queue_split is not None else "library default",
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
@@ -697,11 +807,15 @@ def main():
                                        "note": "rank-0 stream time of the first env-steps after reset"}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": prof_traffic, "traffic_source": traffic_src,
-                         "kernel": batch_kinfo["kernel"] + " + w_env_step_list<128> fallback",
+                         "kernel": batch_kinfo["kernel"] + " + " + full_kinfo.get("kernel", "?") + " fallback",
                          "kernel_ms": step_kernel_ms,
                          "stream_avg_ms": kernel_avg_ms,
                          "kernel_ms_source": "HIP events around the timed region on the library's stream, per "
                                              "step (the step's launches and the gaps between them)",
+                         "kernel_ms_note": "per-step stream time: an upper bound on the dominant kernel's launch "
+                                           "duration, so `achieved` is a lower bound; kernel_ms_instrumented is "
+                                           "the per-step event pair of a window right after (rounds 1-4 divided "
+                                           "by that figure)",
                          "kernel_ms_instrumented": step_kernel_ms_instr,
                          "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
                          "note": "path is FP64-latency-bound (SURVEY.md §8d); HBM fraction reported as required"},

@@ -272,6 +272,15 @@ int ur3e_batch_nu(const ur3e_batch_t* b);
    workgroup, registers per lane */
 int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs);
 
+/* the kernel the handle launches for `tier` (0: the step kernel -- the compact tier, or an untiered
+   layout's only kernel; 1: the grasp tier; 2: the full-capacity fallback tier), chosen by the same
+   branches as ur3e_batch_step: envs resident per CU, LDS bytes per workgroup (static + dynamic),
+   registers per lane, a readable name (name, NUL-terminated within name_len) and the code object's
+   kernel symbol (symbol; empty when the runtime cannot name it).  UR3E_EINVAL for a tier the handle
+   does not launch. */
+int ur3e_batch_tier_kernel(ur3e_batch_t* b, int tier, int* envs_per_cu, int* lds_bytes, int* regs, char* name,
+                           int name_len, char* symbol, int symbol_len);
+
 /* profiling: with timing on (off by default), every ur3e_batch_step that is not being captured into
    a graph records a pair of HIP events around its kernels; last_step_ms reads the most recent pair */
 int ur3e_batch_set_timing(ur3e_batch_t* b, int on);

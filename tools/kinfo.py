@@ -3,37 +3,10 @@ AGPRs, SGPRs, scratch (private segment) bytes per lane, static LDS -- read from 
 metadata note.  usage: python tools/kinfo.py [lib.so] [name-regex]"""
 import os
 import re
-import subprocess
 import sys
-import tempfile
 
-LLVM = "/opt/rocm/lib/llvm/bin"
-
-
-def kernels(lib):
-    with tempfile.TemporaryDirectory() as td:
-        fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "co.o")
-        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
-                        f"--output={co}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
-    out, cur = [], None
-    for line in notes.splitlines():
-        t = line.strip()
-        m = re.match(r"^- \.agpr_count:\s*(\d+)", t)
-        if m:
-            cur = {"agpr": int(m.group(1))}
-            out.append(cur)
-            continue
-        if cur is None:
-            continue
-        for key, name in ((".name:", "name"), (".vgpr_count:", "vgpr"), (".sgpr_count:", "sgpr"),
-                          (".private_segment_fixed_size:", "scratch"), (".group_segment_fixed_size:", "lds"),
-                          (".vgpr_spill_count:", "vgpr_spill"), (".sgpr_spill_count:", "sgpr_spill")):
-            if t.startswith(key):
-                v = t[len(key):].strip()
-                cur[name] = int(v) if v.isdigit() else v
-    return out
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from ur3e_amd.codeobj import kernels  # noqa: E402
 
 
 def main():

@@ -2853,44 +2853,97 @@ extern "C" int ur3e_batch_get_sensordata(ur3e_batch_t* b, double* d_sensordata, 
   return UR3E_OK;
 }
 
-/* resources and occupancy of the step kernel this handle launches (the dominant kernel) */
-extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs) {
-  if (!b) return fail(UR3E_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(b->device));
+/* The kernel a handle launches for one tier, picked by the same branches as launch_tiers and
+   ur3e_batch_step (tier 0: the dominant step kernel -- the compact tier, or the only kernel of an
+   untiered layout; 1: the grasp tier; 2: the full-capacity fallback tier).  fn = null: the handle has
+   no such tier. */
+struct KSel {
   const void* fn;
   int nt;
-  size_t dyn = 0; /* the compact tier's working set is dynamic LDS (w_dyn_lds) */
-  if (b->tiered) {
-    nt = 64;
-    if (b->mesh) {
-      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2>
-           : b->wide ? (const void*)w_env_step<64, KSS_NV_MW, UR3E_TASK_TRAJ_L> : (const void*)w_env_step<64, KSS_NV_M>;
-      dyn = b->wide ? w_dyn_lds<KSS_NV_MW>() : w_dyn_lds<KSS_NV_M>();
-    } else {
-      fn = b->queued ? (const void*)w_env_step_q<64, KSS_NV>
-           : b->wide ? (const void*)w_env_step<64, KSS_NV_W, UR3E_TASK_TRAJ_L>
-           : b->main_tree ? (const void*)w_env_step<64, KSS_NV> : (const void*)w_env_step<64, KSS>;
-      dyn = b->wide ? w_dyn_lds<KSS_NV_W>() : b->main_tree ? w_dyn_lds<KSS_NV>() : w_dyn_lds<KSS>();
-    }
-  } else if (b->wave_nt == 128) {
-    nt = 128;
-    fn = b->mesh ? (const void*)w_env_step<128, KSL_M> : (const void*)w_env_step<128, KSL>;
-  } else if (b->wave_nt == 64) {
-    nt = 64;
-    fn = (const void*)w_env_step<64, KSL>;
-  } else {
-    nt = 64;
-    fn = (const void*)k_env_step;
+  size_t dyn; /* dynamic LDS bytes (the compact tiers' working set, w_dyn_lds) */
+  const char* name;
+};
+#define K_SEL(F, NT, DYN, NAME) KSel{(const void*)(F), (NT), (size_t)(DYN), NAME}
+static KSel step_kernel_sel(const ur3e_batch* b, int tier) {
+  const int task = b->cfg.task;
+  if (!b->tiered) {
+    if (tier != 0) return KSel{nullptr, 0, 0, ""};
+    if (b->wave_nt == 128 && b->mesh) return K_SEL((w_env_step<128, KSL_M>), 128, 0, "w_env_step<128,KSL_M> (full-capacity tier)");
+    if (b->wave_nt == 128) return K_SEL((w_env_step<128, KSL>), 128, 0, "w_env_step<128,KSL> (full-capacity tier)");
+    if (b->wave_nt == 64) return K_SEL((w_env_step<64, KSL>), 64, 0, "w_env_step<64,KSL> (full-capacity tier)");
+    return K_SEL(k_env_step, 64, 0, "k_env_step (one env per lane)");
   }
+  if (tier == 1) {
+    if (!b->grasp) return KSel{nullptr, 0, 0, ""};
+    return b->mesh ? K_SEL((w_env_step_list<64, KSG_NV_M>), 64, 0, "w_env_step_list<64,KSG_NV_M> (grasp tier)")
+                   : K_SEL((w_env_step_list<64, KSG_NV>), 64, 0, "w_env_step_list<64,KSG_NV> (grasp tier)");
+  }
+  if (tier == 2) {
+    if (b->mesh) return K_SEL((w_env_step_list<128, KSL_M>), 128, 0, "w_env_step_list<128,KSL_M> (full-capacity tier)");
+    return K_SEL((w_env_step_list<128, KSL>), 128, 0, "w_env_step_list<128,KSL> (full-capacity tier)");
+  }
+  if (b->mesh) {
+    if (b->queued && task == UR3E_TASK_GYM_V2)
+      return K_SEL((w_env_step_q<64, KSS_NV_M, UR3E_TASK_GYM_V2>), 64, w_dyn_lds<KSS_NV_M>(),
+                   "w_env_step_q<64,KSS_NV_M,GYM_V2> (compact tier, substep work queue)");
+    if (b->queued)
+      return K_SEL((w_env_step_q<64, KSS_NV_M>), 64, w_dyn_lds<KSS_NV_M>(),
+                   "w_env_step_q<64,KSS_NV_M> (compact tier, substep work queue)");
+    if (b->wide)
+      return K_SEL((w_env_step<64, KSS_NV_MW, UR3E_TASK_TRAJ_L>), 64, w_dyn_lds<KSS_NV_MW>(),
+                   "w_env_step<64,KSS_NV_MW,TRAJ_L> (wide compact tier, one workgroup per env-step)");
+    return K_SEL((w_env_step<64, KSS_NV_M>), 64, w_dyn_lds<KSS_NV_M>(),
+                 "w_env_step<64,KSS_NV_M> (compact tier, one workgroup per env-step)");
+  }
+  if (b->queued && task == UR3E_TASK_GYM_V2)
+    return K_SEL((w_env_step_q<64, KSS_NV, UR3E_TASK_GYM_V2>), 64, w_dyn_lds<KSS_NV>(),
+                 "w_env_step_q<64,KSS_NV,GYM_V2> (compact tier, substep work queue)");
+  if (b->queued)
+    return K_SEL((w_env_step_q<64, KSS_NV>), 64, w_dyn_lds<KSS_NV>(),
+                 "w_env_step_q<64,KSS_NV> (compact tier, substep work queue)");
+  if (b->main_tree && task == UR3E_TASK_GYM_V2)
+    return K_SEL((w_env_step<64, KSS_NV, UR3E_TASK_GYM_V2>), 64, w_dyn_lds<KSS_NV>(),
+                 "w_env_step<64,KSS_NV,GYM_V2> (compact tier, one workgroup per env-step)");
+  if (b->main_tree && task == UR3E_TASK_TRAJ_L)
+    return K_SEL((w_env_step<64, KSS_NV_W, UR3E_TASK_TRAJ_L>), 64, w_dyn_lds<KSS_NV_W>(),
+                 "w_env_step<64,KSS_NV_W,TRAJ_L> (wide compact tier, one workgroup per env-step)");
+  if (b->main_tree)
+    return K_SEL((w_env_step<64, KSS_NV>), 64, w_dyn_lds<KSS_NV>(),
+                 "w_env_step<64,KSS_NV> (compact tier, one workgroup per env-step)");
+  return K_SEL((w_env_step<64, KSS>), 64, w_dyn_lds<KSS>(), "w_env_step<64,KSS> (compact tier, one workgroup per env-step)");
+}
+#undef K_SEL
+
+static void copy_cstr(char* dst, int len, const char* src) {
+  if (!dst || len <= 0) return;
+  int i = 0;
+  for (; src && src[i] && i < len - 1; i++) dst[i] = src[i];
+  dst[i] = 0;
+}
+
+extern "C" int ur3e_batch_tier_kernel(ur3e_batch_t* b, int tier, int* envs_per_cu, int* lds_bytes, int* regs,
+                                      char* name, int name_len, char* symbol, int symbol_len) {
+  if (!b) return fail(UR3E_EINVAL, "null handle");
+  if (tier < 0 || tier > 2) return fail(UR3E_EINVAL, "tier must be 0 (step), 1 (grasp) or 2 (full capacity)");
+  const KSel k = step_kernel_sel(b, tier);
+  if (!k.fn) return fail(UR3E_EINVAL, "the handle launches no kernel for this tier");
+  HIPCHK(hipSetDevice(b->device));
   hipFuncAttributes attr;
-  HIPCHK(hipFuncGetAttributes(&attr, fn));
+  HIPCHK(hipFuncGetAttributes(&attr, k.fn));
   int blocks = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, nt, dyn));
-  const int envs = (b->tiered || b->wave_nt) ? blocks : blocks * nt; /* v1: one env per lane */
-  if (envs_per_cu) *envs_per_cu = envs;
-  if (lds_bytes) *lds_bytes = (int)(attr.sharedSizeBytes + dyn);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k.fn, k.nt, k.dyn));
+  const bool lane_per_env = !b->tiered && !b->wave_nt; /* v1: one env per lane */
+  if (envs_per_cu) *envs_per_cu = lane_per_env ? blocks * k.nt : blocks;
+  if (lds_bytes) *lds_bytes = (int)(attr.sharedSizeBytes + k.dyn);
   if (regs) *regs = attr.numRegs;
+  copy_cstr(name, name_len, k.name);
+  if (symbol && symbol_len > 0) copy_cstr(symbol, symbol_len, hipKernelNameRefByPtr(k.fn, nullptr));
   return UR3E_OK;
+}
+
+/* resources and occupancy of the step kernel this handle launches (the dominant kernel) */
+extern "C" int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs) {
+  return ur3e_batch_tier_kernel(b, 0, envs_per_cu, lds_bytes, regs, nullptr, 0, nullptr, 0);
 }
 
 /* diagnostics: per-stage cycle totals of the -DUR3E_STAGE_TIMING build (returns -1 otherwise) */

@@ -1104,9 +1104,11 @@ WD int w_narrow_lds(KS& s, const WPairRow& P, int ln, int slot) {
   const int t1 = P.t1, t2 = P.t2;
   auto& ch = s.kn.chunk();
   const KStageEmit<KS::NPST> emit{&ch.np_stage[0][0], ch.np_key, &ch.np_nstage, ln};
-  /* convex meshes: the mesh-capable layouts settle a pair whose hulls are apart beyond the margin (GJK,
-     or the plane's vertex distances: no contact, the oracle's own decision); a pair that may touch --
-     and every mesh pair in the other layouts -- hands the env-step on to the tier that runs EPA */
+  /* convex meshes: in the mesh-capable layouts (compact and grasp tiers) w_mesh_pass (ur3e_cvx_wave.h)
+     has already settled every mesh pair -- GJK, EPA and plane-convex in the wavefront -- and left its raw
+     contacts in s.kn.mres; they are emitted here at the pair's place in candidate order.  The only hand-offs
+     are an EPA horizon beyond WC_MAXE or more contacts than the layout holds (ovf).  Layouts without
+     meshes never see a mesh pair (the model selects the mesh-capable set) */
   if (t2 == UR3E_GEOM_MESH) {
     if constexpr (KS::MESHES) {
       /* settled by the wave in w_mesh_pass: emit its contacts at the pair's place */

@@ -96,6 +96,8 @@ def _bind(L):
     L.ur3e_batch_queue_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_set_queue_debug.argtypes = [vp, ctypes.c_uint, ip]
     L.ur3e_debug_hold_slots.argtypes = [ip, ip, ip, vp, ctypes.POINTER(ip)]
+    L.ur3e_batch_tier_kernel.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip),
+                                         ctypes.c_char_p, ip, ctypes.c_char_p, ip]
     for f in ("ur3e_batch_num_envs", "ur3e_batch_nq", "ur3e_batch_nv", "ur3e_batch_nu", "ur3e_batch_obs_dim",
               "ur3e_batch_schedule"):
         getattr(L, f).argtypes = [vp]
@@ -374,19 +376,27 @@ class Batch:
         self._chk(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
         return int(v.value)
 
-    SCHEDULES = {0: "w_env_step<64,KSS_NV> (compact tier, one workgroup per env-step)",
-                 1: "w_env_step_q<64,KSS_NV> (compact tier, substep work queue)",
-                 2: "w_env_step<128|64,KSL> (full-capacity tier)", 3: "k_env_step (one env per lane)"}
+    TIERS = {"step": 0, "compact": 0, "grasp": 1, "full": 2}
 
-    def kernel_info(self) -> dict:
-        """{envs_per_cu, lds_bytes, regs, kernel} of the step kernel this handle launches"""
+    def kernel_info(self, tier="step") -> dict:
+        """The kernel this handle launches for `tier` ("step"/"compact": the dominant step kernel; "grasp";
+        "full": the full-capacity fallback), as the library picks it (ur3e_batch_tier_kernel): envs
+        resident per CU, LDS bytes per workgroup, registers per lane, its name and symbol, and the code
+        object's VGPR / AGPR / SGPR counts, scratch bytes and spill counts (ur3e_amd/codeobj.py)."""
         e, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        self._chk(self.L.ur3e_batch_kernel_info(self.h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(r)))
-        name = self.SCHEDULES.get(self.L.ur3e_batch_schedule(self.h), "?")
-        mc = self.model_c
-        if any(mc.geom_type[i] == 7 for i in range(mc.ngeom)):  # the mesh-capable tier set (KSS_NV_M, KSL_M)
-            name = name.replace("KSS_NV>", "KSS_NV_M>").replace("KSL>", "KSL_M>")
-        return {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value, "kernel": name}
+        name, sym = ctypes.create_string_buffer(160), ctypes.create_string_buffer(512)
+        self._chk(self.L.ur3e_batch_tier_kernel(self.h, self.TIERS[tier] if isinstance(tier, str) else int(tier),
+                                                ctypes.byref(e), ctypes.byref(l), ctypes.byref(r), name, 160, sym,
+                                                512))
+        out = {"envs_per_cu": e.value, "lds_bytes": l.value, "regs": r.value, "kernel": name.value.decode(),
+               "symbol": sym.value.decode()}
+        try:
+            from .codeobj import resources
+            res = resources(self.L._name, out["symbol"])
+        except Exception as ex:  # llvm tools missing: the runtime figures above still stand
+            res = {"error": repr(ex)}
+        out["code_object"] = res
+        return out
 
     def set_timing(self, on: bool = True):
         """Record HIP events around every (uncaptured) step, for last_step_ms()."""
