@@ -583,10 +583,17 @@ def main():
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
     ap.add_argument("--launch-timeout", type=float, default=None,
                     help="--gpus N without torchrun: seconds before the rank processes are stopped")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="REHEARSAL ONLY (not a scaling number): let --gpus N ranks share the visible GPUs "
+                         "(rank r on GPU r mod count) over gloo, without the RCCL gather -- exercises the launcher "
+                         "and the multi-rank timing path on a box with fewer GPUs than ranks")
     args = ap.parse_args()
     if launch_mode(args.gpus, os.environ) == "spawn":
         # one process per GPU, started before anything here touches a GPU (this process only counts them)
-        sys.exit(launch_workers(args.gpus, sys.argv[1:], timeout=args.launch_timeout))
+        sys.exit(launch_workers(args.gpus, sys.argv[1:], timeout=args.launch_timeout,
+                                check_devices=not args.rehearse_shared_gpu))
+    if args.rehearse_shared_gpu:
+        args.no_gather = True  # RCCL needs one GPU per rank; gloo has no device gather
 
     import torch
     import torch.distributed as dist
@@ -595,6 +602,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_shared_gpu:
+        local = local % max(torch.cuda.device_count(), 1)
     use_dist = world > 1 or args.gather_self
     if use_dist:
         torch.cuda.set_device(local)
@@ -609,7 +618,10 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if args.rehearse_shared_gpu:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             dist.barrier()
             torch.cuda.synchronize()
         finally:
@@ -797,7 +809,9 @@ def main():
                        "kernel_resources": batch_kinfo,
                        "fallback_kernel_resources": full_kinfo,
                        "queue_split_percent": args.queue_split if args.queue_split is not None else "library default",
-                       "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")},
+                       "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")
+                                      + (" (REHEARSAL: ranks share GPUs over gloo; not a scaling figure)"
+                                         if args.rehearse_shared_gpu else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
             "window": {"pre_steps_untimed": args.pre_steps,
                        "timed_env_steps_since_reset": [args.pre_steps + args.warmup,
