@@ -20,3 +20,6 @@ for P in "LdsLatency" "VmemLatency" \
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $D/p$i -o run -- $B > $D/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $D/p$i.log; exit 1; }
 done
 python3 tools/pmc_breakdown.py $D > /dev/null && echo breakdown ok
+# the C3 scripted pick on main_mesh window by window, with its kernel trace (how the grasp tier shares the time)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/c3trace -o run -- python3 tools/mesh_c3.py 4096 main_mesh > $D/c3_windows.jsonl 2> $D/c3_windows.err || { tail -5 $D/c3_windows.err; exit 1; }
+tail -3 $D/c3_windows.jsonl
