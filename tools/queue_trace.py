@@ -3,7 +3,7 @@ Each (substep, env) unit records when its workgroup pulled it, when its flag wai
 finished (s_memrealtime, 100 MHz).  Per traced launch this prints the span, the mean unit duration per
 substep, the time workgroups spent waiting on flags and between units, and the ideal span (the sum
 of unit run times over the resident workgroups), so the launch's overhead can be told from its work.
-usage: queue_trace.py [n_envs] [steps]"""
+usage: queue_trace.py [n_envs] [steps]   (UR3E_TRACE_MODEL=main_mesh, UR3E_TRACE_PRE=500: the bench's window)"""
 import ctypes, json, os, subprocess, sys
 import numpy as np
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
@@ -23,7 +23,7 @@ if __name__ == "__main__":
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     sched = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     fs = 2
-    md, mc = rt.load_model("main")
+    md, mc = rt.load_model(os.environ.get("UR3E_TRACE_MODEL", "main"))
     b = rt.Batch(mc, rt.make_config(task=rt.TASK_GYM_V2, frame_skip=fs, model=md, seed=1, schedule=sched), n)
     split = int(os.environ.get("UR3E_SPLIT", "-1"))  # percent of each queue's envs split (default: the library's)
     if split >= 0:
@@ -32,7 +32,7 @@ if __name__ == "__main__":
     L = rt.load_library()
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device="cuda")
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device="cuda")
-    for i in range(20):
+    for i in range(int(os.environ.get("UR3E_TRACE_PRE", "20"))):  # untimed env-steps from reset
         b.step(lo + (hi - lo) * torch.rand((n, 4), dtype=torch.float64, device="cuda"))
         torch.cuda.synchronize()
         print("warm-up step", i, flush=True)

@@ -14,7 +14,8 @@ _cache: dict = {}
 
 
 def kernels(lib: str) -> list:
-    """[{name, vgpr, agpr, sgpr, scratch, lds, vgpr_spill, sgpr_spill}, ...] of every kernel in `lib`"""
+    """[{name, vgpr, agpr, sgpr, scratch, lds, vgpr_spill, sgpr_spill, args}, ...] of every kernel in `lib`
+    (args: the kernarg layout, [{offset, size, value_kind}, ...] in parameter order, hidden arguments last)"""
     key = (os.path.abspath(lib), os.path.getmtime(lib))
     if key in _cache:
         return _cache[key]
@@ -27,16 +28,32 @@ def kernels(lib: str) -> list:
                        capture_output=True)
         notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True,
                                check=True).stdout
-    out, cur = [], None
+    out, cur, args_ind = [], None, None
     for line in notes.splitlines():
         t = line.strip()
+        ind = len(line) - len(line.lstrip())
         m = re.match(r"^- \.agpr_count:\s*(\d+)", t)
         if m:
-            cur = {"agpr": int(m.group(1))}
+            cur = {"agpr": int(m.group(1)), "args": []}
             out.append(cur)
+            args_ind = None
             continue
         if cur is None:
             continue
+        if t == ".args:":
+            args_ind = ind
+            continue
+        if args_ind is not None:
+            if ind > args_ind:  # inside the argument list: one "- ." line opens each argument
+                if t.startswith("- "):
+                    cur["args"].append({})
+                    t = t[2:]
+                k, _, v = t.partition(":")
+                if cur["args"] and k in (".offset", ".size", ".value_kind"):
+                    v = v.strip()
+                    cur["args"][-1][k[1:]] = int(v) if v.isdigit() else v
+                continue
+            args_ind = None
         for k, name in ((".name:", "name"), (".vgpr_count:", "vgpr"), (".sgpr_count:", "sgpr"),
                         (".private_segment_fixed_size:", "scratch"), (".group_segment_fixed_size:", "lds"),
                         (".vgpr_spill_count:", "vgpr_spill"), (".sgpr_spill_count:", "sgpr_spill")):

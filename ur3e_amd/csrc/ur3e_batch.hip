@@ -1612,6 +1612,47 @@ WD void w_load_half(const double* __restrict__ half_buf, int e) {
   asm volatile("" ::: "memory");
 }
 
+/* The queue kernel's arguments as they sit in the kernarg segment (the order and natural alignment of its
+   parameter list; checked against the by-value copy at kernel start).  With W_KARG_PTR the kernel reads them
+   through __builtin_amdgcn_kernarg_segment_ptr(), laundered through an empty asm at every unit, so each
+   field is an s_load where it is used.  Read as by-value parameters, every field of KConfig / KState (560
+   bytes) is loaded into SGPRs at kernel entry and kept live across the whole persistent loop: 256 SGPRs
+   spilled to VGPR lanes, reloaded by v_readlane at ~800 sites (the unit's state load and commit, the queue
+   protocol, the controller's gains). */
+struct WQArgs {
+  const ur3e_model_t* m;
+  const KPlan* pl;
+  KConfig c;
+  KState st;
+  const double* actions;
+  int adim;
+  double* obs_out;
+  double* rew_out;
+  unsigned char* term_out;
+  unsigned char* trunc_out;
+  double* tobs_out;
+  int* ovf_list;
+  int* ovf_ctl;
+  int* qctl;
+  int* flags;
+  double* mid;
+  unsigned long long* qstats;
+  double* half_buf;
+};
+static_assert(offsetof(WQArgs, c) == 16 && offsetof(WQArgs, st) == 16 + sizeof(KConfig) &&
+                  offsetof(WQArgs, actions) == offsetof(WQArgs, st) + sizeof(KState),
+              "WQArgs must mirror w_env_step_q's kernarg layout");
+#ifndef W_KARG_PTR
+#define W_KARG_PTR 1
+#endif
+typedef const __attribute__((address_space(4))) WQArgs* WQArgsPtr;
+/* a fresh view of the kernel's arguments: loads through it are not merged with earlier ones */
+__device__ __forceinline__ const WQArgs& w_qargs() {
+  WQArgsPtr p = (WQArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const WQArgs*)p;
+}
+
 template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_model_t* __restrict__ m,
                                                                   const KPlan* __restrict__ pl, KConfig c, KState st,
@@ -1629,20 +1670,37 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
   WOut& o = w_wout<KS>();
   __shared__ int s_u, s_epoch, s_flag, s_from;
   const int tid = threadIdx.x;
+#if W_KARG_PTR
+  /* the parameters are not read by name below (that would load them all at entry): QA(x) reads field x of
+     the unit's fresh argument view U (w_qargs) */
+#define QA(x) U.x
+  const WQArgs& U0 = w_qargs();
+  const int n = U0.st.n, fs = U0.c.frame_skip;
+  const double* const half_buf_ = U0.half_buf;
+  const int split_from_ = U0.c.split_from;
+  const unsigned int spin_cfg_ = U0.c.spin_limit;
+  int* const qctl_ = U0.qctl;
+#else
+#define QA(x) x
   const int n = st.n, fs = c.frame_skip;
+  const double* const half_buf_ = half_buf;
+  const int split_from_ = c.split_from;
+  const unsigned int spin_cfg_ = c.spin_limit;
+  int* const qctl_ = qctl;
+#endif
   /* env partition: XCD-sized queues when n splits evenly, else one queue */
   const int nq = (n & 7) ? 1 : W_NQUEUE;
   const int q = (int)blockIdx.x % nq;
   const int nper = n / nq;
   /* split last substep for the queue's envs [k0, nper): their second halves are queued last */
-  const int k0 = (half_buf && fs >= 2 && fs <= W_FLAG_HALF - 1 && c.split_from < nper)
-                     ? (c.split_from > 0 ? c.split_from : 0) : nper;
+  const int k0 = (half_buf_ && fs >= 2 && fs <= W_FLAG_HALF - 1 && split_from_ < nper)
+                     ? (split_from_ > 0 ? split_from_ : 0) : nper;
   const int nfull = nper * fs;
   const int total = nfull + (nper - k0);
   /* static first units per queue: substep-0 units only */
   const int nstat = min((int)gridDim.x / nq, nper);
-  const unsigned int spin_limit = c.spin_limit ? c.spin_limit : W_SPIN_LIMIT;
-  if (tid == 0) s_epoch = __hip_atomic_load(qctl + W_NQUEUE + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned int spin_limit = spin_cfg_ ? spin_cfg_ : W_SPIN_LIMIT;
+  if (tid == 0) s_epoch = __hip_atomic_load(qctl_ + W_NQUEUE + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   SYNC();
   /* wave-uniform values read from LDS pass through readfirstlane so they live in SGPRs: kept in
      VGPRs across the step they would be spilled (the kernel is at its 256-register budget) */
@@ -1664,6 +1722,9 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
   const int nslot = (int)gridDim.x / nq;
   int next = -1;
   for (;;) {
+#if W_KARG_PTR
+    const WQArgs& U = w_qargs();
+#endif
     int u;
     const int is_static = first;
     if (first) {
@@ -1673,7 +1734,7 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       u = next;
       next = -1;
     } else {
-      if (tid == 0) s_u = atomicAdd(qctl + q, 1);
+      if (tid == 0) s_u = atomicAdd(QA(qctl) + q, 1);
       SYNC();
       u = __builtin_amdgcn_readfirstlane(s_u);
     }
@@ -1690,7 +1751,7 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
       kind = 2;
     }
     const int e0 = q * nper + loc;
-    if (st.route && __builtin_amdgcn_readfirstlane(st.route[e0])) continue; /* stepped by the grasp tier */
+    if (QA(st).route && __builtin_amdgcn_readfirstlane(QA(st).route[e0])) continue; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][0] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1698,11 +1759,11 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
     if (is_static) {
       /* claim the static unit; a consumer may have claimed it (and run it) already */
       if (tid == 0) {
-        const int f = w_flag_poll(flags + e0);
+        const int f = w_flag_poll(QA(flags) + e0);
         int ok = 0;
-        if ((f >> 4) != E && !c.leave_static) {
+        if ((f >> 4) != E && !QA(c).leave_static) {
           int expect = f;
-          ok = __hip_atomic_compare_exchange_strong(flags + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
+          ok = __hip_atomic_compare_exchange_strong(QA(flags) + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         s_flag = ok;
@@ -1712,16 +1773,16 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
     } else if (sub > 0) {
       if (tid == 0) {
         const int want = (E << 4) | (kind == 2 ? W_FLAG_HALF : sub);
-        int f = w_flag_poll(flags + e0);
+        int f = w_flag_poll(QA(flags) + e0);
         int fr = sub;
         /* producer is a static substep-0 unit not claimed yet: claim it and run both substeps */
         if (sub == 1 && u - nper < nstat && (f >> 4) != E) {
           int expect = f;
-          if (__hip_atomic_compare_exchange_strong(flags + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
+          if (__hip_atomic_compare_exchange_strong(QA(flags) + e0, &expect, (E << 4) | W_FLAG_CLAIMED, __ATOMIC_RELAXED,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             fr = 0;
             f = want;
-            atomicAdd(qstats + 1, 1ull);
+            atomicAdd(QA(qstats) + 1, 1ull);
           } else {
             f = expect; /* claimed (or finished) by its owner meanwhile: wait for it below */
           }
@@ -1729,23 +1790,23 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
         unsigned int spins = 0;
         while (f != want && f != bailed) {
           if (++spins > spin_limit) {
-            const int old = atomicExch(flags + e0, bailed);
+            const int old = atomicExch(QA(flags) + e0, bailed);
             if (old == want) {
               f = want; /* released while we gave up: keep going (and keep the flag final) */
-              atomicExch(flags + e0, want);
+              atomicExch(QA(flags) + e0, want);
             } else {
               f = bailed;
               if (old != bailed) {
                 /* the env goes to the fallback tiers, which recompute its env-step (one appender) */
-                atomicAdd(qstats, 1ull);
-                const int slot = atomicAdd(ovf_ctl, 1);
-                if (slot < n) ovf_list[slot] = e0;
+                atomicAdd(QA(qstats), 1ull);
+                const int slot = atomicAdd(QA(ovf_ctl), 1);
+                if (slot < n) QA(ovf_list)[slot] = e0;
               }
             }
             break;
           }
           __builtin_amdgcn_s_sleep(2);
-          f = w_flag_poll(flags + e0);
+          f = w_flag_poll(QA(flags) + e0);
         }
         s_flag = f;
         s_from = fr;
@@ -1759,43 +1820,43 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
     if (W_TRACE_LANES && sub * n + e0 < UR3E_WAVE_TRACE_MAX) ur3e_wave_trace[sub * n + e0][1] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (kind == 2) {
-      w_load_half<KS>(half_buf, e0);
+      w_load_half<KS>(QA(half_buf), e0);
       SYNC();
     }
     const bool ahead = W_CLAIM_AHEAD && u + 2 * nslot < total;
     int nxt = 0;
-    if (ahead && tid == 0) nxt = atomicAdd(qctl + q, 1);
-    const int r0 = kind == 2 ? w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, fs - 1, 1 << 30,
+    if (ahead && tid == 0) nxt = atomicAdd(QA(qctl) + q, 1);
+    const int r0 = kind == 2 ? w_env_step_body<NT, TK>(QA(m), QA(pl), QA(c), QA(st), e0, QA(actions), QA(adim), s, o, fs - 1, 1 << 30,
                                                         nullptr, 2)
-                             : w_env_step_body<NT, TK>(m, pl, c, st, e0, actions, adim, s, o, from,
-                                                        kind ? fs : sub + 1, mid, kind);
+                             : w_env_step_body<NT, TK>(QA(m), QA(pl), QA(c), QA(st), e0, QA(actions), QA(adim), s, o, from,
+                                                        kind ? fs : sub + 1, QA(mid), kind);
     const int r = __builtin_amdgcn_readfirstlane(r0);
     const int e = __builtin_amdgcn_readfirstlane(o.e); /* = e0, reloaded from LDS (see WOut::e) */
     if (r == W_BAIL) {
       if (tid == 0) {
         /* the full-capacity tier recomputes the whole env-step from the committed state */
-        const int old = (sub + 1 < fs || kind == 1) ? atomicExch(flags + e, bailed) : 0;
+        const int old = (sub + 1 < fs || kind == 1) ? atomicExch(QA(flags) + e, bailed) : 0;
         if (old != bailed) {
-          const int slot = atomicAdd(ovf_ctl, 1);
-          if (slot < n) ovf_list[slot] = e;
+          const int slot = atomicAdd(QA(ovf_ctl), 1);
+          if (slot < n) QA(ovf_list)[slot] = e;
         }
       }
     } else if (r == W_HALF) {
-      w_store_half<KS>(half_buf, e);
+      w_store_half<KS>(QA(half_buf), e);
       SYNC();
       if (tid == 0) {
-        const int old = atomicExch(flags + e, (E << 4) | W_FLAG_HALF);
-        if (old == bailed) atomicExch(flags + e, bailed); /* a consumer gave up and claimed the env */
+        const int old = atomicExch(QA(flags) + e, (E << 4) | W_FLAG_HALF);
+        if (old == bailed) atomicExch(QA(flags) + e, bailed); /* a consumer gave up and claimed the env */
       }
     } else if (r == W_PAUSED) {
-      w_store_mid<NT>(m, mid, e, s);
+      w_store_mid<NT>(QA(m), QA(mid), e, s);
       SYNC();
       if (tid == 0) {
-        const int old = atomicExch(flags + e, (E << 4) | (sub + 1));
-        if (old == bailed) atomicExch(flags + e, bailed); /* a consumer gave up and claimed the env */
+        const int old = atomicExch(QA(flags) + e, (E << 4) | (sub + 1));
+        if (old == bailed) atomicExch(QA(flags) + e, bailed); /* a consumer gave up and claimed the env */
       }
     } else {
-      w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+      w_commit<NT, TK>(QA(m), QA(c), QA(st), e, s, o, QA(obs_out), QA(rew_out), QA(term_out), QA(trunc_out), QA(tobs_out), 1);
     }
     if (ahead) {
       if (tid == 0) s_u = nxt;
@@ -1818,12 +1879,13 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
 #endif
   if (tid == 0) {
     __threadfence();
-    if (atomicAdd(qctl + W_NQUEUE, 1) == (int)gridDim.x - 1) {
-      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl + k, k < nq ? nstat : 0);
-      atomicExch(qctl + W_NQUEUE, 0);
-      atomicExch(qctl + W_NQUEUE + 1, E >= 0x7ffffff ? 1 : E + 1); /* never 0: zeroed flags are unclaimed */
+    if (atomicAdd(qctl_ + W_NQUEUE, 1) == (int)gridDim.x - 1) {
+      for (int k = 0; k < W_NQUEUE; k++) atomicExch(qctl_ + k, k < nq ? nstat : 0);
+      atomicExch(qctl_ + W_NQUEUE, 0);
+      atomicExch(qctl_ + W_NQUEUE + 1, E >= 0x7ffffff ? 1 : E + 1); /* never 0: zeroed flags are unclaimed */
     }
   }
+#undef QA
 }
 
 /* a fallback tier over the envs the tier before it queued (grid-stride over the list): the grasp
@@ -1834,8 +1896,14 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
    read it re-zeroes both, so the next step's producer starts from an empty list.  The counters live
    and are reset entirely on the device, so a step captured into a HIP graph replays correctly any
    number of times (no host-side step parity baked into the graph). */
+/* waves per SIMD a list tier is compiled for: two (<= 256 registers) for a 64-lane overlaid layout small
+   enough that more than four fit a CU's 160 KB of LDS (the mesh grasp tier, KSG_NV_M), else one */
 template <int NT, class KS>
-__global__ __launch_bounds__(NT, 1) void w_env_step_list(const ur3e_model_t* __restrict__ m,
+constexpr int w_list_wpe() {
+  return (NT == 64 && KS::OVERLAY && sizeof(KS) + sizeof(WOut) <= 32768) ? 2 : 1;
+}
+template <int NT, class KS>
+__global__ __launch_bounds__(NT, (w_list_wpe<NT, KS>())) void w_env_step_list(const ur3e_model_t* __restrict__ m,
                                                           const KPlan* __restrict__ pl, KConfig c, KState st,
                                                           const double* __restrict__ actions, int adim,
                                                           double* __restrict__ obs_out, double* __restrict__ rew_out,

@@ -446,7 +446,19 @@ typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true> KSG_NV;
    margin themselves (no contact, the oracle's decision with the same code) and hand on an env-step whose
    mesh pair touches; the full-capacity tier runs GJK + EPA */
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSS_NV_M;
-typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
+/* the mesh model's grasp tier: 18 contacts / 72 rows, the most the scripted pick reaches on main.xml with its
+   convex hulls (16 contacts / 62-63 rows in the carry, 17-18 / 65-69 in the grasp and release rows; oracle
+   histogram over the whole trajectory), so the layout is 30.3 KB instead of 36.4 KB and
+   the kernel is built for two waves per SIMD (W_LIST_WPE): five envs per CU instead of four.  A routed
+   carry step (1,136 envs of 4,096) then runs in one round of the grasp kernel's 1,280 slots instead of two
+   rounds of 1,024.  Larger states go on to the full-capacity tier. */
+#ifndef W_GRASP_MESH_MAXCON
+#define W_GRASP_MESH_MAXCON 18
+#endif
+#ifndef W_GRASP_MESH_MAXEFC
+#define W_GRASP_MESH_MAXEFC 72
+#endif
+typedef KSX<W_GRASP_MESH_MAXCON, W_GRASP_MESH_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
 typedef KSX<K_MAXCON, K_MAXEFC, 0, 0, false, K_NG_MESH> KSL_M;
 /* the scripted pick's wider compact tier (10 contacts / 44 rows) with the mesh geoms: its carry rows hold the
    mug on the table, the pads and the closed fingers' linkage meshes (7-8 contacts) */
