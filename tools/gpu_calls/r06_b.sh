@@ -2,7 +2,7 @@
 # round-6 GPU call: the multi-rank bench path rehearsed on one GPU (2 ranks over gloo sharing it: the
 # launcher, shard offsets, barriers and max-over-ranks timing; not a scaling figure), then where the
 # waves of the headline kernel wait (LDS / VMEM latency, instruction mix, active cycles, L1 traffic:
-# one rocprofv3 --pmc pass each, tools/r05_j.sh's groups) -> gpurun_out/$1
+# one rocprofv3 --pmc pass each, tools/gpu_calls/r05_j.sh's groups) -> gpurun_out/$1
 set -o pipefail
 R=$(pwd); D=$R/gpurun_out/$1; mkdir -p $D
 cd /tmp && export TMPDIR=/tmp; cd $R

@@ -1,4 +1,4 @@
-"""Per-launch averages of every counter collected by tools/r05_j.sh for the compact step kernel."""
+"""Per-launch averages of every counter collected by tools/gpu_calls/r05_j.sh for the compact step kernel."""
 import csv, glob, json, os, sys
 
 KEYS = ("w_env_step<64", "w_env_step_q<64")
