@@ -1252,6 +1252,11 @@ __device__ __forceinline__ int* w_near_list(KS& s) {
 #ifndef W_BROAD_2PASS
 #define W_BROAD_2PASS 1
 #endif
+/* the mesh-capable broadphase's pair constants for all its passes loaded ahead of the sphere tests (1) or per
+   pass (0: A/B) */
+#ifndef W_BROAD_AHEAD
+#define W_BROAD_AHEAD 1
+#endif
 template <class KS>
 WD void r_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int lane = w_lane();
@@ -1268,6 +1273,27 @@ WD void r_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {
     int* near = w_near_list(s);
     constexpr int NCAP = KS::NCAND;
     int nnear = 0;
+#if W_BROAD_AHEAD
+    /* every pass's pair constants (the model's pair -> geom chains) issued before the first sphere test, so
+       the passes wait for one round of global loads instead of one per pass */
+    constexpr int NB = (KS::NCAND + 63) / 64;
+    WPairRow PR[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int p = 64 * b + lane;
+      PR[b] = w_pair_row<KS>(m, pl, p < np ? p : 0);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int p = 64 * b + lane;
+      if (64 * b >= np) break;
+      const bool ok = p < np && w_pair_near(s, PR[b]);
+      const unsigned long long bm = __ballot(ok);
+      const int at = nnear + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (ok && at < NCAP) near[at] = p;
+      nnear += __popcll(bm);
+    }
+#else
     for (int base = 0; base < np; base += 64) {
       const int p = base + lane;
       const bool ok = p < np && w_pair_near(s, w_pair_row<KS>(m, pl, p));
@@ -1276,6 +1302,7 @@ WD void r_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {
       if (ok && at < NCAP) near[at] = p;
       nnear += __popcll(bm);
     }
+#endif
     if (nnear > NCAP) nnear = NCAP; /* np <= KS::NCAND (the host checks ncpair): never taken */
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
