@@ -409,6 +409,7 @@ def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500, headline_model
         drv.batch.step(drv.traj.row(t))
     rows = [drv.traj.row(t) for t in range(g0, g1)]
     tc0 = drv.batch.tier_counts()
+    m0 = drv.batch.mid_count()
     it = iter(rows)
     steps_c3 = g1 - g0
     torch.cuda.synchronize()
@@ -419,9 +420,11 @@ def other_configs(n_envs=4096, steps=50, warmup=5, pre_steps=500, headline_model
     e1.record()
     torch.cuda.synchronize()
     tc = [x - y for x, y in zip(drv.batch.tier_counts(), tc0)]
+    mid = drv.batch.mid_count() - m0
     tot = float(n_envs * steps_c3)
     out["C3_main_move_l_mug"] = {"value": n_envs * steps_c3 / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s",
                                  "envs": n_envs, "substeps_per_env_step": 1, "rows": [g0, g1],
+                                 "mid_tier_routed_frac": mid / tot,
                                  # env-steps beyond the compact tier's capacity: routed to the grasp tier by
                                  # the previous step's contact count, or handed on mid-step (and beyond it)
                                  "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot,
@@ -473,6 +476,7 @@ def c3_mesh(n_envs=4096, rows=(1500, 5000)):
         drv.batch.step(drv.traj.row(t))
     rows_t = [drv.traj.row(t) for t in range(g0, g1)]
     tc0 = drv.batch.tier_counts()
+    m0 = drv.batch.mid_count()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -481,11 +485,16 @@ def c3_mesh(n_envs=4096, rows=(1500, 5000)):
     e1.record()
     torch.cuda.synchronize()
     tc = [x - y for x, y in zip(drv.batch.tier_counts(), tc0)]
+    mid = drv.batch.mid_count() - m0
     tot = float(n_envs * (g1 - g0))
     res = {"value": tot / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s", "envs": n_envs,
            "substeps_per_env_step": 1, "rows": [g0, g1], "model": MODEL_VARIANT["main_mesh"],
-           "kernel_resources": drv.batch.kernel_info(), "grasp_kernel_resources": drv.batch.kernel_info("grasp"),
-           "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot}
+           "kernel_resources": drv.batch.kernel_info(), "mid_kernel_resources": drv.batch.kernel_info("mid"),
+           "grasp_kernel_resources": drv.batch.kernel_info("grasp"),
+           "mid_tier_routed_frac": mid / tot,
+           "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
+           "tier_note": "routed env-steps run in the mid tier (16 contacts / 64 rows) when their last forward fits "
+                        "it, else in the grasp tier; the mid tier's bails are counted again in the grasp fraction"}
     drv.close()
     return res
 

@@ -208,6 +208,11 @@ int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
    tier) */
 int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
 
+/* since create (synchronises): env-steps routed to the mid tier (16 contacts / 64 rows), between the compact
+   and the grasp tier -- a routed env whose previous forward fits it runs there, on the same internal stream
+   as the grasp tier and ahead of it; the env-steps it hands on are counted again in tier_counts[2] */
+int ur3e_batch_mid_count(ur3e_batch_t* b, unsigned long long* routed);
+
 /* substep work queue (schedule 1), since create (synchronises): stats[0] units that gave up waiting
    for their producer (spin limit; the env-step then ran in the fallback tiers), stats[1] static
    first units that were claimed and run by their consumer because their own workgroup was not
@@ -273,7 +278,7 @@ int ur3e_batch_nu(const ur3e_batch_t* b);
 int ur3e_batch_kernel_info(ur3e_batch_t* b, int* envs_per_cu, int* lds_bytes, int* regs);
 
 /* the kernel the handle launches for `tier` (0: the step kernel -- the compact tier, or an untiered
-   layout's only kernel; 1: the grasp tier; 2: the full-capacity fallback tier), chosen by the same
+   layout's only kernel; 1: the grasp tier; 2: the full-capacity fallback tier; 3: the mid tier), chosen by the same
    branches as ur3e_batch_step: envs resident per CU, LDS bytes per workgroup (static + dynamic),
    registers per lane, a readable name (name, NUL-terminated within name_len) and the code object's
    kernel symbol (symbol; empty when the runtime cannot name it).  UR3E_EINVAL for a tier the handle

@@ -2,8 +2,9 @@
 against the oracle through the grasp and the carry.  With the stand-in hulls the 2F-85's finger linkage
 meshes interpenetrate once the gripper is closed (a persistent mesh-mesh contact, EPA every row of the
 carry), and the gripper base mesh meets the mug box on the way down; those pairs are settled by the
-wavefront's convex narrowphase in the compact / grasp tiers (ur3e_cvx_wave.h), not handed to the
-full-capacity tier."""
+wavefront's convex narrowphase in the compact / mid / grasp tiers (ur3e_cvx_wave.h), not handed to the
+full-capacity tier.  The carry's 16-contact states run in the mid tier (16 contacts / 64 rows), the grasp
+rows' 17-18-contact states in the grasp tier (18 / 72): every tier of the chain is taken."""
 import numpy as np
 import pytest
 
@@ -43,8 +44,13 @@ def test_move_l_mug_main_mesh_bit_exact():
                 d.forward()
                 mesh_contacts += sum(int(gt[a] == 7 or gt[b] == 7) for a, b in d.contacts()["geoms"])
     tc = gb.tier_counts()
-    print("tier counts (compact->next, full, routed):", tc, "mesh contacts sampled:", mesh_contacts)
+    mid = gb.mid_count()
+    print("tier counts (compact->next, full, routed to grasp):", tc, "routed to mid:", mid,
+          "mesh contacts sampled:", mesh_contacts, "kernels:", gb.kernel_info("mid")["kernel"],
+          gb.kernel_info("grasp")["kernel"])
     assert mesh_contacts > 0
+    # the closed gripper's carry states (16 contacts, 62-63 rows) run in the mid tier
+    assert mid > 0.1 * n * (rows - 1800)
     # the full-capacity tier only sees the compact tier's bails of the few steps before the host turns
     # routing on (round 4: 25 % of the env-steps of this window ran there)
     assert tc[1] <= 0.01 * n * rows

@@ -39,6 +39,6 @@ def test_routing_switches_bit_exact():
         oqp, oqv, ow, onc = ob.get_state()
         assert np.array_equal(qp, oqp) and np.array_equal(qv, oqv) and np.array_equal(w, ow), f"row {t + 1}"
         assert np.array_equal(gb.get_info()["ncon"].cpu().numpy(), onc), f"ncon row {t + 1}"
-        routed_at.append(gb.tier_counts()[2])
-    assert routed_at[-1] > 0, "the grasp rows never routed an env to the grasp tier"
+        routed_at.append(gb.tier_counts()[2] + gb.mid_count())  # routed to the mid or the grasp tier
+    assert routed_at[-1] > 0, "the grasp rows never routed an env past the compact tier"
     drv.close()

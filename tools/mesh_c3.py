@@ -20,6 +20,7 @@ for model in models:
         w1 = min(w1, drv.T)
         rows = [drv.traj.row(t) for t in range(w0, w1)]
         tc0 = drv.batch.tier_counts()
+        m0 = drv.batch.mid_count() if hasattr(drv.batch, "mid_count") else 0
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -29,6 +30,7 @@ for model in models:
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
         tc = [x - y for x, y in zip(drv.batch.tier_counts(), tc0)]
+        mid = (drv.batch.mid_count() if hasattr(drv.batch, "mid_count") else 0) - m0
         k = float(n * (w1 - w0))
         tot_t += ms
         tot_steps += w1 - w0
@@ -36,7 +38,7 @@ for model in models:
         nc = drv.batch.get_info()["ncon"].to(torch.int64)
         print(json.dumps({"model": model, "rows": [w0, w1], "env_steps_per_s": k / (ms * 1e-3),
                           "compact_bail_frac": tc[0] / k, "full_tier_frac": tc[1] / k, "grasp_routed_frac": tc[2] / k,
-                          "ncon_hist_last": {i: v for i, v in enumerate(torch.bincount(nc.clamp(max=40),
+                          "mid_routed_frac": mid / k, "ncon_hist_last": {i: v for i, v in enumerate(torch.bincount(nc.clamp(max=40),
                                                                                        minlength=41).tolist()) if v}}),
               flush=True)
     k = float(n * tot_steps)

@@ -417,7 +417,11 @@ struct KState {
 #endif
 static_assert(W_AHEAD % W_AHEAD_EVERY == 0, "run-ahead bound: a whole number of marker intervals");
 #define W_AHEAD_NEV (W_AHEAD / W_AHEAD_EVERY + 1) /* marker ring: the waited slot is never the one re-recorded */
-#define W_NTOTAL 5 /* device counters of ur3e_batch::d_ovf_total */
+#define W_NTOTAL 6 /* device counters of ur3e_batch::d_ovf_total */
+/* the mid tier (KSM_NV / KSM_NV_M) between the compact and the grasp tier (1, default) or none (0: A/B) */
+#ifndef W_MID_TIER
+#define W_MID_TIER 1
+#endif
 #define W_ROUTE_HOLD 64
 
 struct KConfig {
@@ -438,6 +442,9 @@ struct KConfig {
   /* routing: an env whose committed forward had more contacts or rows than these runs its next step in
      the grasp tier (set at create from the handle's compact-tier capacity) */
   int route_ncon, route_nefc;
+  /* an env routed past the compact tier whose committed forward had no more contacts / rows than these runs
+     in the mid tier, else in the grasp tier (route2_ncon < 0: no mid tier) */
+  int route2_ncon, route2_nefc;
   KGains gains;
 };
 
@@ -983,7 +990,12 @@ WD void w_commit(KModel m, const KConfig& c, const KState& st, int e, const KS& 
   const int od = k_obs_dim(TASK);
   if (tid == 0) {
     st.ncon[e] = s.ncon; st.nwarn[e] = s.nwarn;
-    if (st.hint) st.hint[e] = (unsigned char)(s.ncon > c.route_ncon || s.nefc > c.route_nefc);
+    if (st.hint) {
+      /* 0: the compact tier; 1: the mid tier; 2: the grasp tier */
+      const bool over = s.ncon > c.route_ncon || s.nefc > c.route_nefc;
+      const bool mid = c.route2_ncon >= 0 && s.ncon <= c.route2_ncon && s.nefc <= c.route2_nefc;
+      st.hint[e] = (unsigned char)(over ? (mid ? 1 : 2) : 0);
+    }
     st.t[e] = o.t; st.ep_len[e] = o.ep_len; st.ep_return[e] = o.ep_return; st.episode[e] = o.episode;
     if (stepped && k_is_gym(TASK)) {
       if (rew_out) rew_out[e] = o.r;
@@ -1914,15 +1926,21 @@ __global__ __launch_bounds__(NT, (w_list_wpe<NT, KS>())) void w_env_step_list(co
                                                           unsigned long long* __restrict__ ovf_total,
                                                           int* __restrict__ next_list, int* next_ctl,
                                                           int* __restrict__ pred_list, int* pred_ctl,
-                                                          unsigned long long* __restrict__ ovf_total2 = nullptr) {
+                                                          unsigned long long* __restrict__ ovf_total2,
+                                                          int* __restrict__ predm_list, int* predm_ctl) {
   __shared__ KS s;
   __shared__ WOut o;
-  __shared__ int s_cnt;
+  __shared__ int s_cnt, s_cntm;
   if (pred_list && blockIdx.x == 0) {
     /* the last kernel of the step: snapshot the routing hints for the next step and list the routed
-       envs for its grasp-tier pre-pass (the order of the list does not matter: envs are independent) */
-    if (threadIdx.x == 0) s_cnt = 0;
+       envs for its pre-passes -- hint 1 the mid tier's list (predm, when there is one), hint 2 the grasp
+       tier's (the order of a list does not matter: envs are independent) */
+    if (threadIdx.x == 0) { s_cnt = 0; s_cntm = 0; }
     SYNC();
+    auto put = [&](int e, unsigned int h) {
+      if (h == 1u && predm_list) predm_list[atomicAdd(&s_cntm, 1)] = e;
+      else pred_list[atomicAdd(&s_cnt, 1)] = e;
+    };
     /* 16 envs per thread and load (4,096 envs: two passes of the workgroup instead of 32 dependent
        byte loads per thread) */
     const int n16 = st.n >> 4;
@@ -1931,19 +1949,23 @@ __global__ __launch_bounds__(NT, (w_list_wpe<NT, KS>())) void w_env_step_list(co
       ((uint4*)st.route)[c] = h;
       if (h.x | h.y | h.z | h.w) {
         const unsigned int w[4] = {h.x, h.y, h.z, h.w};
-        for (int k = 0; k < 16; k++)
-          if ((w[k >> 2] >> (8 * (k & 3))) & 0xffu) pred_list[atomicAdd(&s_cnt, 1)] = 16 * c + k;
+        for (int k = 0; k < 16; k++) {
+          const unsigned int hk = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+          if (hk) put(16 * c + k, hk);
+        }
       }
     }
     for (int e = 16 * n16 + threadIdx.x; e < st.n; e += NT) {
       const unsigned char h = st.hint[e];
       st.route[e] = h;
-      if (h) pred_list[atomicAdd(&s_cnt, 1)] = e;
+      if (h) put(e, h);
     }
     SYNC();
     if (threadIdx.x == 0) {
       __hip_atomic_store(pred_ctl, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (st.routed_host) __hip_atomic_store(st.routed_host, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (predm_ctl) __hip_atomic_store(predm_ctl, s_cntm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st.routed_host)
+        __hip_atomic_store(st.routed_host, s_cnt + s_cntm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     SYNC();
   }
@@ -2067,8 +2089,9 @@ struct ur3e_batch {
   int* d_ovf_list;
   int* d_ovf_ctl; /* {count, blocks_done}: device-resident, reset by w_env_step_list */
   unsigned long long* d_ovf_total; /* [0] env-steps the compact tier handed on, [1] the grasp tier,
-                                      [2] routed to the grasp tier, [3] queue give-ups, [4] static
-                                      queue units claimed by their consumer */
+                                      [2] routed to the grasp tier (with the mid tier's bails), [3] queue
+                                      give-ups, [4] static queue units claimed by their consumer, [5] routed
+                                      to the mid tier */
   int grasp;       /* the tiers are compact -> grasp (KSG_NV) -> full capacity (main.xml only) */
   int* h_routed;   /* host-mapped routed-env count of the last route snapshot (KState.routed_host) */
   int g_grid;      /* resident workgroups of the grasp-tier list kernel */
@@ -2076,6 +2099,11 @@ struct ur3e_batch {
   int* d_ovf2_ctl;
   int* d_pred_list; /* envs routed to the grasp tier for the next step (route snapshot) */
   int* d_pred_ctl;
+  int midt;          /* the mid tier (KSM_NV / KSM_NV_M) between the compact and the grasp tier */
+  int m_grid;        /* resident workgroups of the mid-tier list kernel */
+  int* d_predm_list; /* envs routed to the mid tier for the next step (route snapshot); its bails join
+                        d_pred_list for the grasp pre-pass after it */
+  int* d_predm_ctl;
   hipStream_t side; /* the grasp-tier pre-pass runs here, concurrently with the compact tier */
   hipEvent_t ev_fork, ev_join;
   /* bounded run-ahead (grasp tier on): step k (a multiple of W_AHEAD_EVERY) waits for step k - W_AHEAD to
@@ -2413,6 +2441,11 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->wide = tiered && main_tree && cfg->task == UR3E_TASK_TRAJ_L;
   c.route_ncon = b->wide ? W_WIDE_MAXCON - 2 : W_SMALL_MAXCON - 1;
   c.route_nefc = b->wide ? W_WIDE_MAXEFC - 8 : W_SMALL_MAXEFC - 3;
+  /* routed envs whose last forward fits the mid tier run there (no margin below its capacity: the states
+     it serves -- a closed grasp, the carry -- hold their contact set from step to step; one that outgrows it
+     bails to the grasp tier); set below once the handle's tiers are known */
+  c.route2_ncon = -1;
+  c.route2_nefc = -1;
   for (int k = 0; k < 12; k++) {
     c.gains.task[k] = cfg->task_gains[k];
     c.gains.joint[k] = cfg->joint_gains[k];
@@ -2461,6 +2494,7 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
   b->grasp = tiered && b->main_tree;
   b->d_ovf2_list = nullptr; b->d_ovf2_ctl = nullptr; b->g_grid = 0;
   b->d_pred_list = nullptr; b->d_pred_ctl = nullptr; b->side = nullptr;
+  b->midt = 0; b->m_grid = 0; b->d_predm_list = nullptr; b->d_predm_ctl = nullptr;
   s.hint = nullptr; s.route = nullptr; s.routed_host = nullptr; b->h_routed = nullptr;
   b->hstep = 0; b->last_route = -1;
   if (b->grasp) {
@@ -2477,6 +2511,21 @@ extern "C" int ur3e_batch_create(const ur3e_model_t* model, const ur3e_config_t*
     HIPCHK(hipMalloc(&b->d_pred_list, sizeof(int) * nd));
     HIPCHK(hipMalloc(&b->d_pred_ctl, 2 * sizeof(int)));
     HIPCHK(hipMemset(b->d_pred_ctl, 0, 2 * sizeof(int)));
+    /* the mid tier (a positive diagnostic contact cap keeps the three-tier chain it tests) */
+    b->midt = W_MID_TIER && cfg->tier_con_cap <= 0;
+    if (b->midt) {
+      int mper = 0;
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &mper, b->mesh ? (const void*)w_env_step_list<64, KSM_NV_M> : (const void*)w_env_step_list<64, KSM_NV>, 64, 0));
+      b->m_grid = mper * cus;
+      if (b->m_grid < 1) b->m_grid = 1;
+      if (b->m_grid > n_envs) b->m_grid = n_envs;
+      HIPCHK(hipMalloc(&b->d_predm_list, sizeof(int) * nd));
+      HIPCHK(hipMalloc(&b->d_predm_ctl, 2 * sizeof(int)));
+      HIPCHK(hipMemset(b->d_predm_ctl, 0, 2 * sizeof(int)));
+      b->cfg.route2_ncon = W_MID_MAXCON;
+      b->cfg.route2_nefc = W_MID_MAXEFC - 1;
+    }
     HIPCHK(hipMalloc(&s.hint, nd));
     HIPCHK(hipMemset(s.hint, 0, nd));
     HIPCHK(hipMalloc(&s.route, nd));
@@ -2561,6 +2610,8 @@ extern "C" int ur3e_batch_destroy(ur3e_batch_t* b) {
   if (b->d_ovf2_ctl) (void)hipFree(b->d_ovf2_ctl);
   if (b->d_pred_list) (void)hipFree(b->d_pred_list);
   if (b->d_pred_ctl) (void)hipFree(b->d_pred_ctl);
+  if (b->d_predm_list) (void)hipFree(b->d_predm_list);
+  if (b->d_predm_ctl) (void)hipFree(b->d_predm_ctl);
   if (b->st.hint) (void)hipFree(b->st.hint);
   if (b->st.route) (void)hipFree(b->st.route);
   if (b->h_routed) (void)hipHostFree(b->h_routed);
@@ -2603,7 +2654,7 @@ extern "C" int ur3e_batch_reset(ur3e_batch_t* b, const uint8_t* d_mask, double* 
 /* the tiered step's launches for one tier set (compact KSC, grasp KSG, full capacity KSF): the grasp
    pre-pass (pre), the compact tier, the grasp tier over the compact tier's bails, the full-capacity tier
    over the grasp tier's (or, without the grasp tier, the compact tier's) */
-template <class KSC, class KSG, class KSF, class KSW>
+template <class KSC, class KSG, class KSF, class KSW, class KSM>
 static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool pre, const double* d_actions, int adim,
                         double* d_obs, double* d_reward, uint8_t* d_terminated, uint8_t* d_truncated,
                         double* d_terminal_obs) {
@@ -2620,10 +2671,16 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
        the compact tier (which skips them) runs here */
     HIPCHK(hipEventRecord(b->ev_fork, st));
     HIPCHK(hipStreamWaitEvent(b->side, b->ev_fork, 0));
+    /* the mid tier first: the envs it cannot hold join the grasp tier's list, which runs after it */
+    if (b->midt)
+      hipLaunchKernelGGL((w_env_step_list<64, KSM>), dim3(b->m_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
+                         b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
+                         b->d_predm_list, b->d_predm_ctl, b->d_ovf_total + 5, b->d_pred_list, b->d_pred_ctl,
+                         nullptr, nullptr, nullptr, nullptr, nullptr);
     hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, b->side, b->d_model, b->d_plan,
                        b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                        b->d_pred_list, b->d_pred_ctl, b->d_ovf_total + 2, b->d_ovf2_list, b->d_ovf2_ctl,
-                       nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipEventRecord(b->ev_join, b->side));
   }
   /* main.xml: dof count and tree specialised at compile time; the gym ur3e-v2 and scripted
@@ -2682,18 +2739,19 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
       hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                          b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                          b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, b->d_ovf2_list, b->d_ovf2_ctl, nullptr,
-                         nullptr, nullptr);
+                         nullptr, nullptr, nullptr, nullptr);
     }
     /* the full-capacity tier, whose workgroup 0 also snapshots the routing hints for the next step;
        fed by the compact tier directly (routing off), its count is the compact tier's hand-on too */
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                        b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
-                       b->d_pred_ctl, direct ? b->d_ovf_total : nullptr);
+                       b->d_pred_ctl, direct ? b->d_ovf_total : nullptr, b->d_predm_list, b->d_predm_ctl);
   } else {
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
-                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       b->d_ovf_list, b->d_ovf_ctl, b->d_ovf_total, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, nullptr);
   }
   return UR3E_OK;
 }
@@ -2738,9 +2796,9 @@ extern "C" int ur3e_batch_step(ur3e_batch_t* b, const double* d_actions, int adi
       pre = capturing || (b->last_route >= 0 && b->hstep - b->last_route < W_ROUTE_HOLD);
       if (!pre) kst.route = nullptr;
     }
-    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M, KSS_NV_MW>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+    const int rc = b->mesh ? launch_tiers<KSS_NV_M, KSG_NV_M, KSL_M, KSS_NV_MW, KSM_NV_M>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                       d_terminated, d_truncated, d_terminal_obs)
-                           : launch_tiers<KSS_NV, KSG_NV, KSL, KSS_NV_W>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
+                           : launch_tiers<KSS_NV, KSG_NV, KSL, KSS_NV_W, KSM_NV>(b, st, kst, pre, d_actions, adim, d_obs, d_reward,
                                                                 d_terminated, d_truncated, d_terminal_obs);
     if (rc != UR3E_OK) return rc;
   } else if (b->wave_nt == 128 && b->mesh)
@@ -2946,6 +3004,11 @@ static KSel step_kernel_sel(const ur3e_batch* b, int tier) {
     return b->mesh ? K_SEL((w_env_step_list<64, KSG_NV_M>), 64, 0, "w_env_step_list<64,KSG_NV_M> (grasp tier)")
                    : K_SEL((w_env_step_list<64, KSG_NV>), 64, 0, "w_env_step_list<64,KSG_NV> (grasp tier)");
   }
+  if (tier == 3) {
+    if (!b->midt) return KSel{nullptr, 0, 0, ""};
+    return b->mesh ? K_SEL((w_env_step_list<64, KSM_NV_M>), 64, 0, "w_env_step_list<64,KSM_NV_M> (mid tier)")
+                   : K_SEL((w_env_step_list<64, KSM_NV>), 64, 0, "w_env_step_list<64,KSM_NV> (mid tier)");
+  }
   if (tier == 2) {
     if (b->mesh) return K_SEL((w_env_step_list<128, KSL_M>), 128, 0, "w_env_step_list<128,KSL_M> (full-capacity tier)");
     return K_SEL((w_env_step_list<128, KSL>), 128, 0, "w_env_step_list<128,KSL> (full-capacity tier)");
@@ -2992,7 +3055,7 @@ static void copy_cstr(char* dst, int len, const char* src) {
 extern "C" int ur3e_batch_tier_kernel(ur3e_batch_t* b, int tier, int* envs_per_cu, int* lds_bytes, int* regs,
                                       char* name, int name_len, char* symbol, int symbol_len) {
   if (!b) return fail(UR3E_EINVAL, "null handle");
-  if (tier < 0 || tier > 2) return fail(UR3E_EINVAL, "tier must be 0 (step), 1 (grasp) or 2 (full capacity)");
+  if (tier < 0 || tier > 3) return fail(UR3E_EINVAL, "tier must be 0 (step), 1 (grasp), 2 (full capacity) or 3 (mid)");
   const KSel k = step_kernel_sel(b, tier);
   if (!k.fn) return fail(UR3E_EINVAL, "the handle launches no kernel for this tier");
   HIPCHK(hipSetDevice(b->device));
@@ -3067,6 +3130,14 @@ extern "C" int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* count
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(counts, b->d_ovf_total, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return UR3E_OK;
+}
+
+extern "C" int ur3e_batch_mid_count(ur3e_batch_t* b, unsigned long long* routed) {
+  if (!b || !routed) return fail(UR3E_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(routed, b->d_ovf_total + 5, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return UR3E_OK;
 }
 

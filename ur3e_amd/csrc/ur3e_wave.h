@@ -459,6 +459,20 @@ typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KS
 #define W_GRASP_MESH_MAXEFC 72
 #endif
 typedef KSX<W_GRASP_MESH_MAXCON, W_GRASP_MESH_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
+/* mid tier, between the compact and the grasp tier: 16 contacts / 64 rows -- one constraint row per lane, so
+   the register solver of the compact tier (RPL 1) instead of the grasp tier's two rows per lane -- in a 25.2 KB
+   layout built for two waves per SIMD: six envs per CU.  It takes the routed env-steps that fit it, which on
+   the scripted pick are the closed gripper's carry states (16 contacts, 62-63 rows, 28 % of the envs; the
+   grasp tier's 18/72 and 24/96 run them at five and four per CU with twice the row work per lane); its bails
+   join the grasp tier's pre-pass list. */
+#ifndef W_MID_MAXCON
+#define W_MID_MAXCON 16
+#endif
+#ifndef W_MID_MAXEFC
+#define W_MID_MAXEFC 64
+#endif
+typedef KSX<W_MID_MAXCON, W_MID_MAXEFC, UR3E_MAIN_NV, 1, true> KSM_NV;
+typedef KSX<W_MID_MAXCON, W_MID_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSM_NV_M;
 typedef KSX<K_MAXCON, K_MAXEFC, 0, 0, false, K_NG_MESH> KSL_M;
 /* the scripted pick's wider compact tier (10 contacts / 44 rows) with the mesh geoms: its carry rows hold the
    mug on the table, the pads and the closed fingers' linkage meshes (7-8 contacts) */
@@ -1252,10 +1266,11 @@ __device__ __forceinline__ int* w_near_list(KS& s) {
 #ifndef W_BROAD_2PASS
 #define W_BROAD_2PASS 1
 #endif
-/* the mesh-capable broadphase's pair constants for all its passes loaded ahead of the sphere tests (1) or per
-   pass (0: A/B) */
+/* the mesh-capable broadphase's pair constants for all its passes loaded ahead of the sphere tests (1: A/B) or
+   per pass (0, default).  Dropped: same-box A/B 8.806 against 8.815 M env-steps/s (profiles/r06_ab A/B 2) --
+   the model constants' load latency is not on the wave's critical path here */
 #ifndef W_BROAD_AHEAD
-#define W_BROAD_AHEAD 1
+#define W_BROAD_AHEAD 0
 #endif
 template <class KS>
 WD void r_collision(KModel m, const KPlan* __restrict__ pl, KS& s) {

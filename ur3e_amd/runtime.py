@@ -94,6 +94,7 @@ def _bind(L):
     L.ur3e_batch_get_task_space_state.argtypes = [vp, vp, vp]
     L.ur3e_batch_get_actuator_force.argtypes = [vp, vp, vp]
     L.ur3e_batch_queue_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ur3e_batch_mid_count.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.ur3e_batch_set_queue_debug.argtypes = [vp, ctypes.c_uint, ip]
     L.ur3e_debug_hold_slots.argtypes = [ip, ip, ip, vp, ctypes.POINTER(ip)]
     L.ur3e_batch_tier_kernel.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip),
@@ -353,6 +354,13 @@ class Batch:
         self._chk(self.L.ur3e_batch_tier_counts(self.h, v))
         return int(v[0]), int(v[1]), int(v[2])
 
+    def mid_count(self) -> int:
+        """Since create: env-steps routed to the mid tier (16 contacts / 64 rows, between the compact and the
+        grasp tier); its bails are counted again in tier_counts()[2]."""
+        v = ctypes.c_ulonglong()
+        self._chk(self.L.ur3e_batch_mid_count(self.h, ctypes.byref(v)))
+        return int(v.value)
+
     def queue_stats(self) -> tuple:
         """Since create, substep work queue: (units that gave up waiting for their producer, static first
         units claimed and run by their consumer)."""
@@ -376,10 +384,10 @@ class Batch:
         self._chk(self.L.ur3e_batch_overflow_count(self.h, ctypes.byref(v)))
         return int(v.value)
 
-    TIERS = {"step": 0, "compact": 0, "grasp": 1, "full": 2}
+    TIERS = {"step": 0, "compact": 0, "grasp": 1, "full": 2, "mid": 3}
 
     def kernel_info(self, tier="step") -> dict:
-        """The kernel this handle launches for `tier` ("step"/"compact": the dominant step kernel; "grasp";
+        """The kernel this handle launches for `tier` ("step"/"compact": the dominant step kernel; "mid"; "grasp";
         "full": the full-capacity fallback), as the library picks it (ur3e_batch_tier_kernel): envs
         resident per CU, LDS bytes per workgroup, registers per lane, its name and symbol, and the code
         object's VGPR / AGPR / SGPR counts, scratch bytes and spill counts (ur3e_amd/codeobj.py)."""
