@@ -128,6 +128,15 @@ def launch_workers(n: int, argv, script: str | None = None, check_devices: bool 
     return rc
 
 
+def _kinfo(batch, tier="step"):
+    """kernel_info of one tier, or None when the handle does not launch that tier (e.g. a build without the mid
+    tier)"""
+    try:
+        return batch.kernel_info(tier)
+    except RuntimeError:
+        return None
+
+
 def _profile_file(kind: str):
     """profiles/<kind>_rNN.json of the newest round that has one (traffic: PMC HBM bytes per launch of
     the step kernel; flops: the oracle-counted FP64 flops per env-step), or None.  Each file records the
@@ -489,8 +498,8 @@ def c3_mesh(n_envs=4096, rows=(1500, 5000)):
     tot = float(n_envs * (g1 - g0))
     res = {"value": tot / (e0.elapsed_time(e1) * 1e-3), "unit": "env-steps/s", "envs": n_envs,
            "substeps_per_env_step": 1, "rows": [g0, g1], "model": MODEL_VARIANT["main_mesh"],
-           "kernel_resources": drv.batch.kernel_info(), "mid_kernel_resources": drv.batch.kernel_info("mid"),
-           "grasp_kernel_resources": drv.batch.kernel_info("grasp"),
+           "kernel_resources": drv.batch.kernel_info(), "mid_kernel_resources": _kinfo(drv.batch, "mid"),
+           "grasp_kernel_resources": _kinfo(drv.batch, "grasp"),
            "mid_tier_routed_frac": mid / tot,
            "grasp_tier_routed_frac": tc[2] / tot, "compact_bail_frac": tc[0] / tot, "full_tier_frac": tc[1] / tot,
            "tier_note": "routed env-steps run in the mid tier (16 contacts / 64 rows) when their last forward fits "
@@ -648,10 +657,7 @@ def main():
     if args.queue_split is not None:
         batch.set_queue_split(args.queue_split)
     batch_kinfo = batch.kernel_info()
-    try:
-        full_kinfo = batch.kernel_info("full")
-    except RuntimeError:  # an untiered layout has no fallback tier
-        full_kinfo = {}
+    full_kinfo = _kinfo(batch, "full") or {}  # an untiered layout has no fallback tier
     lo = torch.tensor([0.04799994, -0.11650084, 0.0, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([0.54799994, 0.38349916, 0.5, 1.0], dtype=torch.float64, device=dev)
     gen = torch.Generator(device=dev)

@@ -1657,13 +1657,15 @@ static_assert(offsetof(WQArgs, c) == 16 && offsetof(WQArgs, st) == 16 + sizeof(K
 #ifndef W_KARG_PTR
 #define W_KARG_PTR 1
 #endif
-typedef const __attribute__((address_space(4))) WQArgs* WQArgsPtr;
-/* a fresh view of the kernel's arguments: loads through it are not merged with earlier ones */
-__device__ __forceinline__ const WQArgs& w_qargs() {
-  WQArgsPtr p = (WQArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+/* a fresh view of the running kernel's arguments as the struct A that mirrors its parameter list: loads
+   through it are not merged with earlier ones */
+template <class A>
+__device__ __forceinline__ const A& w_kargs() {
+  const __attribute__((address_space(4))) A* p = (const __attribute__((address_space(4))) A*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
-  return *(const WQArgs*)p;
+  return *(const A*)p;
 }
+__device__ __forceinline__ const WQArgs& w_qargs() { return w_kargs<WQArgs>(); }
 
 template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_model_t* __restrict__ m,
@@ -1908,6 +1910,39 @@ __global__ __launch_bounds__(NT, W_WPE_OF(KS)) void w_env_step_q(const ur3e_mode
    read it re-zeroes both, so the next step's producer starts from an empty list.  The counters live
    and are reset entirely on the device, so a step captured into a HIP graph replays correctly any
    number of times (no host-side step parity baked into the graph). */
+/* w_env_step_list's arguments as they sit in the kernarg segment (see WQArgs): with W_KARG_LIST the
+   per-env loop reads them through a fresh kernarg view per env instead of keeping all of KConfig / KState
+   in SGPRs across it (265-298 SGPRs spilled to VGPR lanes in the list tiers) */
+struct WLArgs {
+  const ur3e_model_t* m;
+  const KPlan* pl;
+  KConfig c;
+  KState st;
+  const double* actions;
+  int adim;
+  double* obs_out;
+  double* rew_out;
+  unsigned char* term_out;
+  unsigned char* trunc_out;
+  double* tobs_out;
+  const int* ovf_list;
+  int* ovf_ctl;
+  unsigned long long* ovf_total;
+  int* next_list;
+  int* next_ctl;
+  int* pred_list;
+  int* pred_ctl;
+  unsigned long long* ovf_total2;
+  int* predm_list;
+  int* predm_ctl;
+};
+static_assert(offsetof(WLArgs, c) == 16 && offsetof(WLArgs, st) == 16 + sizeof(KConfig) &&
+                  offsetof(WLArgs, actions) == offsetof(WLArgs, st) + sizeof(KState),
+              "WLArgs must mirror w_env_step_list's kernarg layout");
+#ifndef W_KARG_LIST
+#define W_KARG_LIST 1
+#endif
+
 /* waves per SIMD a list tier is compiled for: two (<= 256 registers) for a 64-lane overlaid layout small
    enough that more than four fit a CU's 160 KB of LDS (the mesh grasp tier, KSG_NV_M), else one */
 template <int NT, class KS>
@@ -1988,20 +2023,27 @@ __global__ __launch_bounds__(NT, (w_list_wpe<NT, KS>())) void w_env_step_list(co
   SYNC();
   const int cnt = s_cnt;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const int e = ovf_list[i];
+#if W_KARG_LIST
+    const WLArgs& U = w_kargs<WLArgs>();
+#define LA(x) U.x
+#else
+#define LA(x) x
+#endif
+    const int e = LA(ovf_list)[i];
     WT_INIT();
-    const int r = w_env_step_body<NT>(m, pl, c, st, e, actions, adim, s, o);
+    const int r = w_env_step_body<NT>(LA(m), LA(pl), LA(c), LA(st), e, LA(actions), LA(adim), s, o);
     WT_FLUSH();
     if (r == W_BAIL) {
       if constexpr (KS::BAIL) {
         if (threadIdx.x == 0) {
-          const int slot = atomicAdd(next_ctl, 1);
-          if (slot < st.n) next_list[slot] = e;
+          const int slot = atomicAdd(LA(next_ctl), 1);
+          if (slot < LA(st).n) LA(next_list)[slot] = e;
         }
       }
     } else {
-      w_commit<NT>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+      w_commit<NT>(LA(m), LA(c), LA(st), e, s, o, LA(obs_out), LA(rew_out), LA(term_out), LA(trunc_out), LA(tobs_out), 1);
     }
+#undef LA
     SYNC();
   }
 }

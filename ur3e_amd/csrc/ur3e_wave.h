@@ -446,17 +446,16 @@ typedef KSX<W_GRASP_MAXCON, W_GRASP_MAXEFC, UR3E_MAIN_NV, 1, true> KSG_NV;
    margin themselves (no contact, the oracle's decision with the same code) and hand on an env-step whose
    mesh pair touches; the full-capacity tier runs GJK + EPA */
 typedef KSX<W_SMALL_MAXCON, W_SMALL_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSS_NV_M;
-/* the mesh model's grasp tier: 18 contacts / 72 rows, the most the scripted pick reaches on main.xml with its
-   convex hulls (16 contacts / 62-63 rows in the carry, 17-18 / 65-69 in the grasp and release rows; oracle
-   histogram over the whole trajectory), so the layout is 30.3 KB instead of 36.4 KB and
-   the kernel is built for two waves per SIMD (W_LIST_WPE): five envs per CU instead of four.  A routed
-   carry step (1,136 envs of 4,096) then runs in one round of the grasp kernel's 1,280 slots instead of two
-   rounds of 1,024.  Larger states go on to the full-capacity tier. */
+/* the mesh model's grasp tier.  18 contacts / 72 rows (30.3 KB, built for two waves per SIMD: five envs per CU
+   instead of four) was measured +2.7 % on the C3 mesh pick without the mid tier (profiles/r06_ab A/B 1), but
+   the scripted pick's grasp rows reach beyond it in a few envs (the full-capacity tier took 0.1 % of rows
+   2,100-2,600, which cost that window 12 %); with the mid tier taking the carry's 16-contact states, the grasp
+   tier only serves the rarer larger ones, so it keeps the box model's 24 / 96 (A/B 3) */
 #ifndef W_GRASP_MESH_MAXCON
-#define W_GRASP_MESH_MAXCON 18
+#define W_GRASP_MESH_MAXCON W_GRASP_MAXCON
 #endif
 #ifndef W_GRASP_MESH_MAXEFC
-#define W_GRASP_MESH_MAXEFC 72
+#define W_GRASP_MESH_MAXEFC W_GRASP_MAXEFC
 #endif
 typedef KSX<W_GRASP_MESH_MAXCON, W_GRASP_MESH_MAXEFC, UR3E_MAIN_NV, 1, true, K_NG_MESH> KSG_NV_M;
 /* mid tier, between the compact and the grasp tier: 16 contacts / 64 rows -- one constraint row per lane, so
