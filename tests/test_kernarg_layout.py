@@ -1,4 +1,4 @@
-"""The substep-queue kernel and the list tiers read their own arguments through __builtin_amdgcn_kernarg_segment_ptr() as a
+"""The substep-queue kernel, the list tiers and the per-env-step kernels read their own arguments through __builtin_amdgcn_kernarg_segment_ptr() as a
 WQArgs struct (ur3e_batch.hip, W_KARG_PTR: fields loaded where used instead of all at entry, which had kept
 560 bytes of KConfig / KState in SGPRs and spilled 256 of them).  That is only right while the compiler lays
 the explicit kernel arguments out as C lays out a struct of the same members: each at the next offset
@@ -16,9 +16,10 @@ LIB = os.path.join(REPO, "ur3e_amd", "_lib", "libur3e_amd.so")
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
-@pytest.mark.parametrize("prefix,nargs", [("_Z12w_env_step_q", 18), ("_Z15w_env_step_list", 21)])
+@pytest.mark.parametrize("prefix,nargs", [("_Z12w_env_step_q", 18), ("_Z15w_env_step_list", 21),
+                                          ("_Z10w_env_stepI", 13)])
 def test_kernel_kernarg_layout_is_the_struct_layout(prefix, nargs):
-    """the queue kernel (WQArgs) and the list tiers (WLArgs)"""
+    """the queue kernel (WQArgs), the list tiers (WLArgs) and the per-env-step kernels (WEArgs)"""
     from ur3e_amd.codeobj import kernels
     qs = [k for k in kernels(LIB) if k.get("name", "").startswith(prefix)]
     assert qs, f"no {prefix} kernel in the library"

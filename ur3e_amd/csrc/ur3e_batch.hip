@@ -1502,6 +1502,39 @@ KD int k_xcd_env(int b, int n) {
   return (b & 7) * (n >> 3) + (b >> 3);
 }
 
+/* a fresh view of the running kernel's arguments as the struct A that mirrors its parameter list: loads
+   through it are not merged with earlier ones */
+template <class A>
+__device__ __forceinline__ const A& w_kargs() {
+  const __attribute__((address_space(4))) A* p = (const __attribute__((address_space(4))) A*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const A*)p;
+}
+
+/* w_env_step's arguments as they sit in the kernarg segment (see WQArgs): with W_KARG_STEP the kernel reads
+   them through the kernarg view where they are used instead of all at entry */
+struct WEArgs {
+  const ur3e_model_t* m;
+  const KPlan* pl;
+  KConfig c;
+  KState st;
+  const double* actions;
+  int adim;
+  double* obs_out;
+  double* rew_out;
+  unsigned char* term_out;
+  unsigned char* trunc_out;
+  double* tobs_out;
+  int* ovf_list;
+  int* ovf_count;
+};
+static_assert(offsetof(WEArgs, c) == 16 && offsetof(WEArgs, st) == 16 + sizeof(KConfig) &&
+                  offsetof(WEArgs, actions) == offsetof(WEArgs, st) + sizeof(KState),
+              "WEArgs must mirror w_env_step's kernarg layout");
+#ifndef W_KARG_STEP
+#define W_KARG_STEP 1
+#endif
+
 template <int NT, class KS, int TK = -1>
 __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_step(const ur3e_model_t* __restrict__ m, const KPlan* __restrict__ pl,
                                                   KConfig c, KState st, const double* __restrict__ actions, int adim,
@@ -1512,24 +1545,39 @@ __global__ __launch_bounds__(NT, (KS::OVERLAY ? W_WPE_OF(KS) : 1)) void w_env_st
                                                   int* __restrict__ ovf_count) {
   KS& s = w_smem<KS>();
   WOut& o = w_wout<KS>();
-  if ((int)blockIdx.x >= st.n) return;
-  const int e = k_xcd_env((int)blockIdx.x, st.n);
-  if (st.route && __builtin_amdgcn_readfirstlane(st.route[e])) return; /* stepped by the grasp tier */
+#if W_KARG_STEP
+  const WEArgs& U = w_kargs<WEArgs>();
+#define EA(x) U.x
+#else
+#define EA(x) x
+#endif
+  if ((int)blockIdx.x >= EA(st).n) return;
+  const int e = k_xcd_env((int)blockIdx.x, EA(st).n);
+  if (EA(st).route && __builtin_amdgcn_readfirstlane(EA(st).route[e])) return; /* stepped by the grasp tier */
 #ifdef UR3E_WAVE_TRACE
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   WT_INIT();
-  if (w_env_step_body<NT, TK>(m, pl, c, st, e, actions, adim, s, o) == W_BAIL) {
+  if (w_env_step_body<NT, TK>(EA(m), EA(pl), EA(c), EA(st), e, EA(actions), EA(adim), s, o) == W_BAIL) {
     if (threadIdx.x == 0) {
       /* each env is appended at most once per step and the fallback kernel re-zeroes the counter,
          so the slot is < n; the bound check keeps a corrupted counter from writing out of range */
-      const int slot = atomicAdd(ovf_count, 1);
-      if (slot < st.n) ovf_list[slot] = e;
+      const WEArgs& V = w_kargs<WEArgs>();
+      const int slot = atomicAdd(W_KARG_STEP ? V.ovf_count : ovf_count, 1);
+      if (slot < EA(st).n) (W_KARG_STEP ? V.ovf_list : ovf_list)[slot] = e;
     }
     WT_FLUSH();
     return;
   }
+#if W_KARG_STEP
+  {
+    const WEArgs& V = w_kargs<WEArgs>(); /* a fresh view: the commit's pointers are loaded here, not kept */
+    w_commit<NT, TK>(V.m, V.c, V.st, e, s, o, V.obs_out, V.rew_out, V.term_out, V.trunc_out, V.tobs_out, 1);
+  }
+#else
   w_commit<NT, TK>(m, c, st, e, s, o, obs_out, rew_out, term_out, trunc_out, tobs_out, 1);
+#endif
+#undef EA
   WT(27);
   WT_FLUSH();
 #ifdef UR3E_WAVE_TRACE
@@ -1657,14 +1705,6 @@ static_assert(offsetof(WQArgs, c) == 16 && offsetof(WQArgs, st) == 16 + sizeof(K
 #ifndef W_KARG_PTR
 #define W_KARG_PTR 1
 #endif
-/* a fresh view of the running kernel's arguments as the struct A that mirrors its parameter list: loads
-   through it are not merged with earlier ones */
-template <class A>
-__device__ __forceinline__ const A& w_kargs() {
-  const __attribute__((address_space(4))) A* p = (const __attribute__((address_space(4))) A*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return *(const A*)p;
-}
 __device__ __forceinline__ const WQArgs& w_qargs() { return w_kargs<WQArgs>(); }
 
 template <int NT, class KS, int TK = -1>
