@@ -665,10 +665,20 @@ def main():
 
     gather = use_dist and not args.no_gather
     if gather:
-        # double-buffered payload: step t's gather runs on its own stream while step t+1 computes
+        # double-buffered payload: step t's gather runs on its own stream while step t+1 computes.  The env step
+        # writes its outputs straight into the payload (obs [n, 24], reward [n], then terminated and truncated as
+        # bytes), so one gather sends it whole with no packing kernels on the env stream; buffer k is rewritten
+        # only after the gather that last read it (two steps earlier) has completed (its event)
         comm = torch.cuda.Stream(device=dev)
-        payloads = [torch.empty((n, 26), dtype=torch.float64, device=dev) for _ in range(2)]
+        od = batch.obs_dim
+        plen = n * od + n + (2 * n + 7) // 8
+        payloads = [torch.empty(plen, dtype=torch.float64, device=dev) for _ in range(2)]
+        outs = []
+        for p_ in payloads:
+            fl = p_[n * od + n:].view(torch.uint8)
+            outs.append((p_[:n * od].view(n, od), p_[n * od:n * od + n], fl[:n], fl[n:2 * n]))
         glists = [[torch.empty_like(payloads[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+        gdone = [None, None]
         nstep = [0]
 
     step_events = []
@@ -684,22 +694,24 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        obs, rew, term, trunc, _ = batch.step(a)
+        if gather:
+            k = nstep[0] & 1
+            nstep[0] += 1
+            if gdone[k] is not None:  # the gather that last read this buffer (two steps ago)
+                torch.cuda.current_stream().wait_event(gdone[k])
+            batch.step(a, out=outs[k])
+        else:
+            batch.step(a)
         if timed:
             e1.record()
             step_events.append((e0, e1))
         if gather:
-            k = nstep[0] & 1
-            nstep[0] += 1
-            payload = payloads[k]
-            # the gather that last read this buffer (two steps ago) must be done before it is refilled
-            torch.cuda.current_stream().wait_stream(comm)
-            payload[:, :24] = obs
-            payload[:, 24] = rew
-            payload[:, 25] = (term | trunc).to(torch.float64)
             comm.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(comm):
-                dist.gather(payload, glists[k], dst=0)
+                dist.gather(payloads[k], glists[k], dst=0)
+                ev = torch.cuda.Event()
+                ev.record()
+            gdone[k] = ev
 
     # (1) fresh-reset window (secondary figure): the first n_fresh env-steps after reset, timed on the
     # stream; (2) the rest of the --pre-steps, untimed, so the headline window is mid-episode
@@ -744,6 +756,18 @@ def main():
         one_step(acts[args.warmup + args.steps + i], timed=True)
     torch.cuda.synchronize()
     step_kernel_ms_instr = sum(a.elapsed_time(b) for a, b in step_events) / len(step_events)
+    gather_check = None
+    if gather and rank == 0:
+        # the last gathered payload's rank-0 slot is this rank's payload, bit for bit, and decodes to the step's
+        # outputs (obs rows, reward, terminated / truncated bytes) -- the layout the policy rank reads
+        torch.cuda.synchronize()
+        kl = (nstep[0] - 1) & 1
+        got = glists[kl][0]
+        o_, r_, te_, tr_ = outs[kl]
+        fl = got[n * od + n:].view(torch.uint8)
+        gather_check = bool(torch.equal(got, payloads[kl]) and torch.equal(got[:n * od].view(n, od), o_)
+                            and torch.equal(got[n * od:n * od + n], r_) and torch.equal(fl[:n], te_)
+                            and torch.equal(fl[n:2 * n], tr_))
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -828,6 +852,9 @@ def main():
                                       + (" (REHEARSAL: ranks share GPUs over gloo; not a scaling figure)"
                                          if args.rehearse_shared_gpu else "")},
             "fallback_env_steps_frac": fallback / float(n * args.steps),
+            "gather": ({"payload_doubles_per_rank": plen, "layout": "obs [n, obs_dim] | reward [n] | terminated, "
+                        "truncated bytes [2n], written by the env step in place", "rank0_slot_check": gather_check}
+                       if gather else None),
             "window": {"pre_steps_untimed": args.pre_steps,
                        "timed_env_steps_since_reset": [args.pre_steps + args.warmup,
                                                        args.pre_steps + args.warmup + args.steps],

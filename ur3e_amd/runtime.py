@@ -264,12 +264,24 @@ class Batch:
         self._chk(self.L.ur3e_batch_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()))
         return self.obs
 
-    def step(self, actions):
+    def step(self, actions, out=None):
+        """One env-step of every env.  `out` = (obs [n, obs_dim] f64, reward [n] f64, terminated [n] u8,
+        truncated [n] u8) device tensors the library writes instead of the handle's own buffers (e.g. views
+        of one payload a collective then sends whole); each is checked before the launch."""
         a = actions.to(device=self.device, dtype=self.torch.float64).contiguous()
-        self._chk(self.L.ur3e_batch_step(self.h, _ptr(a), a.shape[1], _ptr(self.obs), _ptr(self.reward),
-                                      _ptr(self.terminated), _ptr(self.truncated), _ptr(self.terminal_obs),
-                                      self._stream()))
-        return self.obs, self.reward, self.terminated, self.truncated, self.terminal_obs
+        if out is None:
+            obs, rew, term, trunc = self.obs, self.reward, self.terminated, self.truncated
+        else:
+            obs, rew, term, trunc = out
+            t = self.torch
+            for x, shape, dt, what in ((obs, (self.n, self.obs_dim), t.float64, "obs"), (rew, (self.n,), t.float64, "reward"),
+                                       (term, (self.n,), t.uint8, "terminated"), (trunc, (self.n,), t.uint8, "truncated")):
+                if not isinstance(x, t.Tensor) or x.device != self.device or x.dtype != dt or tuple(x.shape) != shape \
+                        or not x.is_contiguous():
+                    raise ValueError(f"step: out {what} must be a contiguous {dt} tensor of shape {shape} on {self.device}")
+        self._chk(self.L.ur3e_batch_step(self.h, _ptr(a), a.shape[1], _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+                                      _ptr(self.terminal_obs), self._stream()))
+        return obs, rew, term, trunc, self.terminal_obs
 
     def get_state(self):
         t = self.torch
