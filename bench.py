@@ -599,6 +599,9 @@ def main():
                          "reference's collision set); main: main.xml's box-surrogate compile")
     ap.add_argument("--gather-self", action="store_true",
                     help="init RCCL and run the gather path even at one rank (exercises the overlap logic)")
+    ap.add_argument("--env-priority", choices=["auto", "normal", "high"], default="auto",
+                    help="priority of the stream the env steps run on; auto: high when the RCCL gather runs beside "
+                         "them (its kernels then take the slots the env kernel's tail leaves), else normal")
     ap.add_argument("--launch-timeout", type=float, default=None,
                     help="--gpus N without torchrun: seconds before the rank processes are stopped")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
@@ -681,6 +684,13 @@ def main():
         gdone = [None, None]
         nstep = [0]
 
+    env_priority = args.env_priority if args.env_priority != "auto" else ("high" if gather else "normal")
+    if env_priority == "high":
+        # the env steps on a high-priority stream: the dispatcher then places the env kernel's workgroups ahead
+        # of the gather's, which runs in the slots the env kernel's tail frees
+        torch.cuda.synchronize()
+        lo_p, hi_p = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=min(lo_p, hi_p)))
     step_events = []
     # synthetic inputs are generated before the timed regions and stay resident in HBM (one [n, 4]
     # action batch per step); the timed loops run only the env step (and the gather)
@@ -848,6 +858,7 @@ def main():
                        "kernel_resources": batch_kinfo,
                        "fallback_kernel_resources": full_kinfo,
                        "queue_split_percent": args.queue_split if args.queue_split is not None else "library default",
+                       "env_stream_priority": env_priority,
                        "parallelism": f"env-shard{world}" + ("+rccl-gather" if gather else "")
                                       + (" (REHEARSAL: ranks share GPUs over gloo; not a scaling figure)"
                                          if args.rehearse_shared_gpu else "")},
