@@ -55,3 +55,34 @@ def test_move_l_mug_main_mesh_bit_exact():
     # routing on (round 4: 25 % of the env-steps of this window ran there)
     assert tc[1] <= 0.01 * n * rows
     drv.close()
+
+
+def test_mid_tier_bails_through_the_chain_bit_exact():
+    """A diagnostic contact cap (tier_con_cap -12 caps every bailing tier at 12 contacts) makes the mid tier
+    hand its 13-16-contact envs on: they join the grasp tier's list behind it on the side stream, the grasp
+    tier (capped too) hands them to the full-capacity tier -- the whole chain compact -> mid -> grasp -> full,
+    bit-exact against the oracle through the grasp rows."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import pyoracle as po
+    from ur3e_amd.controller.move_l_mug import MoveLMug
+    n, rows = 64, 2600
+    drv = MoveLMug(n, reset_mode="low", seed=0, model="main_mesh", tier_con_cap=-12)
+    gb = drv.batch
+    ob = po.OracleBatch(gb.model_c, po.config_from(gb.cfg), n)
+    for t in range(rows):
+        row = drv.step()
+        ob.step(row.cpu().numpy())
+        if t % 650 == 649:
+            torch.cuda.synchronize()
+            qp, qv, wa = gb.get_state()
+            oqp, oqv, owa, onc = ob.get_state()
+            np.testing.assert_array_equal(qp.cpu().numpy(), oqp, err_msg=f"qpos row {t}")
+            np.testing.assert_array_equal(qv.cpu().numpy(), oqv, err_msg=f"qvel row {t}")
+            np.testing.assert_array_equal(wa.cpu().numpy(), owa, err_msg=f"warm start row {t}")
+            np.testing.assert_array_equal(gb.get_info()["ncon"].cpu().numpy(), onc, err_msg=f"ncon row {t}")
+    tc, mid = gb.tier_counts(), gb.mid_count()
+    print("tier counts (compact->next, full, routed to grasp):", tc, "routed to mid:", mid)
+    assert mid > 0 and tc[2] > 0 and tc[1] > 0  # every tier of the chain was taken
+    drv.close()
