@@ -418,6 +418,11 @@ struct KState {
 static_assert(W_AHEAD % W_AHEAD_EVERY == 0, "run-ahead bound: a whole number of marker intervals");
 #define W_AHEAD_NEV (W_AHEAD / W_AHEAD_EVERY + 1) /* marker ring: the waited slot is never the one re-recorded */
 #define W_NTOTAL 6 /* device counters of ur3e_batch::d_ovf_total */
+/* the compact tier's bails straight to the full-capacity tier while routing is on too (1) or to the grasp
+   tier behind it (0) -- A/B */
+#ifndef W_DIRECT_PRE
+#define W_DIRECT_PRE 1
+#endif
 /* the mid tier (KSM_NV / KSM_NV_M) between the compact and the grasp tier (1, default) or none (0: A/B) */
 #ifndef W_MID_TIER
 #define W_MID_TIER 1
@@ -2744,8 +2749,12 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
   /* routing off (no pre-pass): the grasp tier is not launched at all -- the compact tier's rare bails
      go straight to the full-capacity tier, which every env fits, and the step is two launches instead
      of three (an empty grasp-tier launch cost ~1.4 % of the step) */
-  const bool direct = b->grasp && !pre && b->cfg.tier_con_cap <= 0; /* a positive diagnostic cap keeps the
-                                                                        grasp tier behind the compact one */
+  /* with routing on as well (W_DIRECT_PRE): the compact tier's bails -- a few per million env-steps once the
+     routed envs run ahead of it -- go straight to the full-capacity tier too, and the serial (nearly always
+     empty) grasp-tier launch behind the compact one is dropped; the full-capacity list then also takes the
+     bails of the side stream's mid / grasp chain, which the step joins before it */
+  const bool direct = b->grasp && (!pre || W_DIRECT_PRE) && b->cfg.tier_con_cap <= 0; /* a positive diagnostic
+                                                                        cap keeps the grasp tier behind the compact one */
   int* const c_list = direct ? b->d_ovf2_list : b->d_ovf_list;
   int* const c_ctl = direct ? b->d_ovf2_ctl : b->d_ovf_ctl;
   if (pre) {
@@ -2828,7 +2837,7 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
                        b->d_ovf2_list, b->d_ovf2_ctl, b->d_ovf_total + 1, nullptr, nullptr, b->d_pred_list,
-                       b->d_pred_ctl, direct ? b->d_ovf_total : nullptr, b->d_predm_list, b->d_predm_ctl);
+                       b->d_pred_ctl, (direct && !pre) ? b->d_ovf_total : nullptr, b->d_predm_list, b->d_predm_ctl);
   } else {
     hipLaunchKernelGGL((w_env_step_list<128, KSF>), dim3(grid), dim3(128), 0, st, b->d_model, b->d_plan, b->cfg,
                        b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
