@@ -2824,8 +2824,11 @@ static int launch_tiers(ur3e_batch* b, hipStream_t st, const KState& kst, bool p
                        d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs, c_list, c_ctl);
   int grid = b->n < W_FULL_GRID ? b->n : W_FULL_GRID;
   if (b->grasp) {
+    /* join the pre-pass before anything reads its bails or hints: the grasp tier behind the compact one, or
+       (direct) the full-capacity tier, whose list the side stream's chain appends to and whose workgroup 0
+       snapshots the hints that chain commits */
+    if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0));
     if (!direct) {
-      if (pre) HIPCHK(hipStreamWaitEvent(st, b->ev_join, 0)); /* join the pre-pass */
       /* compact-tier bails -> grasp tier; grasp-tier bails (both passes) -> full-capacity tier */
       hipLaunchKernelGGL((w_env_step_list<64, KSG>), dim3(b->g_grid), dim3(64), 0, st, b->d_model, b->d_plan,
                          b->cfg, b->st, d_actions, adim, d_obs, d_reward, d_terminated, d_truncated, d_terminal_obs,
