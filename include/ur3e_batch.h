@@ -200,13 +200,12 @@ int ur3e_batch_get_ctrl(ur3e_batch_t* b, double* d_ctrl, void* stream);
 /* env-steps the compact tier handed on to the fallback tiers since create (synchronises) */
 int ur3e_batch_overflow_count(ur3e_batch_t* b, unsigned long long* total);
 
-/* since create (synchronises): counts[0] env-steps the compact tier handed on while routing is off (straight
-   to the full-capacity tier; with a positive diagnostic tier_con_cap, to the grasp tier in every step),
-   counts[1] env-steps that reached the full-capacity tier (while routing is on, the compact tier's rare bails
-   go there directly and are counted here only), counts[2] env-steps routed to the grasp tier (the env's
-   previous forward exceeded the compact tier's routing thresholds, 4 / 27 for the gym tasks and 8 / 36 for
-   the scripted pick, and the mid tier's 16 / 63 -- or it bailed from the mid tier; it runs on an internal
-   stream concurrently with the compact tier) */
+/* since create (synchronises): counts[0] env-steps the compact tier handed on (to the grasp tier while
+   routing is in use, else straight to the full-capacity tier), counts[1] env-steps that reached the
+   full-capacity tier, counts[2] env-steps routed to the grasp tier (the env's previous forward exceeded the
+   compact tier's routing thresholds, 4 / 27 for the gym tasks and 8 / 36 for the scripted pick, and the mid
+   tier's 16 / 63 -- or it bailed from the mid tier; it runs on an internal stream concurrently with the
+   compact tier) */
 int ur3e_batch_tier_counts(ur3e_batch_t* b, unsigned long long* counts);
 
 /* since create (synchronises): env-steps routed to the mid tier (16 contacts / 64 rows), between the compact

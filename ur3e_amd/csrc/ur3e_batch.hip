@@ -419,9 +419,10 @@ static_assert(W_AHEAD % W_AHEAD_EVERY == 0, "run-ahead bound: a whole number of 
 #define W_AHEAD_NEV (W_AHEAD / W_AHEAD_EVERY + 1) /* marker ring: the waited slot is never the one re-recorded */
 #define W_NTOTAL 6 /* device counters of ur3e_batch::d_ovf_total */
 /* the compact tier's bails straight to the full-capacity tier while routing is on too (1) or to the grasp
-   tier behind it (0) -- A/B */
+   tier behind it (0, default): one serial launch fewer per routed step, but the scripted pick's compact bails
+   then run at one env per 128-lane workgroup -- C3 box -1.5 %, the rest neutral (profiles/r06_ab A/B 6) */
 #ifndef W_DIRECT_PRE
-#define W_DIRECT_PRE 1
+#define W_DIRECT_PRE 0
 #endif
 /* the mid tier (KSM_NV / KSM_NV_M) between the compact and the grasp tier (1, default) or none (0: A/B) */
 #ifndef W_MID_TIER
