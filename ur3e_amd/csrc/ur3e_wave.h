@@ -34,6 +34,16 @@
    more hands on to the next tier */
 #define W_MAXSURV 64
 #define W_MAXGRP 96   /* constraint row groups */
+/* the overlaid layouts' row groups beyond their contacts (equality and frictionloss groups of the plan, active
+   joint limits): an env-step with more groups than MAXCON + this hands on to the next tier (r_mc_layout) */
+#ifndef W_GRP_EXTRA
+#define W_GRP_EXTRA 24
+#endif
+/* the overlaid layouts keep the rows' R / D / aref, the Newton Hessian and the solved forces in one union
+   of the constraint area (1, default) or side by side (0: A/B) -- 2 KB less for 64 rows */
+#ifndef W_ROWS_IN_HL
+#define W_ROWS_IN_HL 1
+#endif
 /* compact-tier narrowphase: survivor lanes per chunk (their clip polygons live in LDS) and staged
    raw contacts per chunk (>= the compact tier's MAXCON: a chunk staging more has overflowed) */
 #define W_NP_LANES 8
@@ -194,6 +204,7 @@ struct KSX;
 template <int MC, int ME, int NVC, int TREE, int NGC>
 struct KSX<MC, ME, NVC, TREE, false, NGC> {
   static constexpr bool OVERLAY = false;
+  static constexpr bool RHL = false; /* separate row arrays (see the overlaid layout) */
   /* geoms this layout holds; NGC = K_NG_MESH: the mesh-capable variant (main.xml with real meshes) */
   static constexpr int NG = NGC;
   static constexpr bool MESHES = NGC == K_NG_MESH;
@@ -288,10 +299,16 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
   static constexpr int STATIC_TREE = TREE;
   static constexpr int MAXCON = MC;
   static constexpr int MAXEFC = ME;
-  static constexpr int MAXGRP = ME < W_MAXGRP ? ME : W_MAXGRP;
+  /* each group holds a row, so ME bounds the groups; in the layouts of 64+ rows (whose LDS bounds their envs
+     per CU) so do the contacts plus W_GRP_EXTRA (r_mc_layout bails beyond it) */
+  static constexpr int MAXGRP0 = ME < W_MAXGRP ? ME : W_MAXGRP;
+  static constexpr int MAXGRP = (ME >= 64 && MC + W_GRP_EXTRA < MAXGRP0) ? MC + W_GRP_EXTRA : MAXGRP0;
   static constexpr bool BAIL = (MC < K_MAXCON) || (ME < K_MAXEFC);
   /* constraint rows per lane of the register solver: row r lives on lane r % 64, slot r / 64 */
   static constexpr int RPL = (ME + 63) / 64;
+  /* the rows' R / D / aref, Hl and the solved forces share bytes (W_ROWS_IN_HL) in the layouts whose envs
+     per CU their LDS bounds (the mid and grasp tiers, 64+ rows); the compact tiers are bound by registers */
+  static constexpr bool RHL = W_ROWS_IN_HL && ME >= 64;
   /* raw contacts one narrowphase chunk may stage (a chunk staging more has overflowed MAXCON) */
   static constexpr int NPST = MC > W_NP_STAGE ? MC : W_NP_STAGE;
   static_assert(RPL <= 2 && MC <= 64, "the register solver holds at most two rows per lane");
@@ -347,11 +364,20 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
     };
     struct { /* N */
       double efc_J[ME][K_NV];
-      double efc_R[ME], efc_D[ME], efc_aref[ME], efc_force[ME];
       int efc_type[ME], efc_id[ME], efc_grp[ME];
       int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
       double con_Hc[MC][9];
-      double Hl[K_NV * (K_NV + 1) / 2];
+      /* RHL: by lifetime, the rows' regulariser, its inverse and reference acceleration from
+         w_make_constraint until r_load_rows copies them into the solver's registers; then the Newton
+         Hessian, its factor and (RPL 1) the ordered-sum slots; then the solved forces, which only the touch
+         sensors read before the implicit-damping tree solve reuses the bytes.  The smooth acceleration's
+         tree solve, which uses Hl too, then runs before the rows are made (w_forward).  Without RHL the
+         three lie side by side (the pads are empty with it) */
+      union {
+        struct { double efc_R[ME], efc_D[ME], efc_aref[ME]; };
+        struct { double rhl_pad0_[RHL ? 0 : 3 * ME]; double Hl[K_NV * (K_NV + 1) / 2]; };
+        struct { double rhl_pad1_[RHL ? 0 : 3 * ME + K_NV * (K_NV + 1) / 2]; double efc_force[ME]; };
+      };
       /* ordered-sum slots of the register solver when rows span two lanes' slots (RPL 2); with
          RPL 1 the three 64-double slots live in Hl (see R_SLOT) */
       double rslot[RPL > 1 ? 3 * 64 * RPL : 1];
@@ -2544,6 +2570,15 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0, b
   W_DBL(4, w_collision<NT>(m, pl, s));
   WT(4);
   if (KS::BAIL && s.ovf) return;
+  if constexpr (REG && KS::RHL) {
+    /* the smooth acceleration before the constraint rows (it reads neither): its tree solve's LDS transpose
+       shares bytes with the rows' R / D / aref (KSX::RHL) */
+    double x;
+    W_DBL(8, x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0));
+    if (tid < nv) s.qacc_smooth[tid] = x;
+    SYNC();
+    WT(8);
+  }
   W_DBL(5, w_make_constraint<NT>(m, pl, s));
   WT(5);
   if (KS::BAIL && s.ovf) return;
@@ -2554,15 +2589,16 @@ WD void w_forward(KModel m, const KPlan* __restrict__ pl, KS& s, int part = 0, b
     w_rne_passive<NT>(m, pl, s);
     WT(7);
   }
-  if constexpr (REG) {
+  if constexpr (REG && !KS::RHL) {
     double x;
     W_DBL(8, x = r_tree_solve(m, pl, s, false, tid < nv ? s.qfrc_smooth[tid] : 0.0));
     if (tid < nv) s.qacc_smooth[tid] = x;
     SYNC();
-  } else {
+    WT(8);
+  } else if constexpr (!REG) {
     w_solve_tree<NT>(m, pl, s.H, s.LDinv, s.qacc_smooth, s.qfrc_smooth);
+    WT(8);
   }
-  WT(8);
   if (REG && part == 1) return;
   }
 solve:

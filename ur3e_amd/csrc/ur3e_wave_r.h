@@ -1015,6 +1015,15 @@ WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
   RRow W[RPL];
 #pragma unroll
   for (int h = 0; h < RPL; h++) r_load_rows(m, s, W[h], lane + 64 * h);
+  /* the rows' R / D / aref share bytes with Hl and the ordered-sum slots (W_ROWS_IN_HL): read before any
+     of those is written */
+#ifndef W_LOAD_FENCE
+#define W_LOAD_FENCE 1
+#endif
+  if (W_LOAD_FENCE && KS::RHL) {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
   double Ma, gauss, cost;
   RDBL(22, r_eval_state(m, s, W, qacc, qs, qas, Ma, gauss, cost));
   const double cost_ws = cost;
@@ -1772,8 +1781,11 @@ WD void r_mc_layout(KModel m, const KPlan* __restrict__ pl, KS& s) {
   const int ncg = __popcll(mc);
   const int nrow = nfixrow + nlim + 3 * ncg;
   const int ngrp = nfix + nlim + ncg;
-  /* rows beyond the tier's capacity, or more groups than lanes (lane = group below), bail */
-  if (nrow > KS::MAXEFC || ngrp > 64) {
+  /* rows beyond the tier's capacity, or more groups than lanes (lane = group below) or than the layout
+     holds (KSX::MAXGRP), bail */
+  static_assert(KS::BAIL, "the overlaid layouts hand on what they cannot hold");
+  constexpr int GMAX = KS::MAXGRP < 64 ? KS::MAXGRP : 64;
+  if (nrow > KS::MAXEFC || ngrp > GMAX) {
     if (lane == 0) s.ovf = 1;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
