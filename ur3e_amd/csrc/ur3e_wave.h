@@ -35,14 +35,17 @@
 #define W_MAXSURV 64
 #define W_MAXGRP 96   /* constraint row groups */
 /* the overlaid layouts' row groups beyond their contacts (equality and frictionloss groups of the plan, active
-   joint limits): an env-step with more groups than MAXCON + this hands on to the next tier (r_mc_layout) */
+   joint limits): with W_ROWS_IN_HL, an env-step with more groups than MAXCON + this hands on to the next tier
+   (r_mc_layout) */
 #ifndef W_GRP_EXTRA
 #define W_GRP_EXTRA 24
 #endif
-/* the overlaid layouts keep the rows' R / D / aref, the Newton Hessian and the solved forces in one union
-   of the constraint area (1, default) or side by side (0: A/B) -- 2 KB less for 64 rows */
+/* the 64+-row overlaid layouts keep the rows' R / D / aref, the Newton Hessian and the solved forces in one
+   union of the constraint area, and their group arrays sized by contacts (1), or side by side (0, default).
+   1 takes the mid tier from 25.2 to 22.9 KB of LDS, seven envs per CU instead of six, bit-exact, and measured
+   0.6-1.2 % slower on the scripted pick (profiles/r06_ab A/B 7): its envs fit the chip at six per CU already */
 #ifndef W_ROWS_IN_HL
-#define W_ROWS_IN_HL 1
+#define W_ROWS_IN_HL 0
 #endif
 /* compact-tier narrowphase: survivor lanes per chunk (their clip polygons live in LDS) and staged
    raw contacts per chunk (>= the compact tier's MAXCON: a chunk staging more has overflowed) */
@@ -299,10 +302,10 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
   static constexpr int STATIC_TREE = TREE;
   static constexpr int MAXCON = MC;
   static constexpr int MAXEFC = ME;
-  /* each group holds a row, so ME bounds the groups; in the layouts of 64+ rows (whose LDS bounds their envs
-     per CU) so do the contacts plus W_GRP_EXTRA (r_mc_layout bails beyond it) */
+  /* each group holds a row, so ME bounds the groups; with W_ROWS_IN_HL, in the layouts of 64+ rows, so do the
+     contacts plus W_GRP_EXTRA (r_mc_layout bails beyond it) */
   static constexpr int MAXGRP0 = ME < W_MAXGRP ? ME : W_MAXGRP;
-  static constexpr int MAXGRP = (ME >= 64 && MC + W_GRP_EXTRA < MAXGRP0) ? MC + W_GRP_EXTRA : MAXGRP0;
+  static constexpr int MAXGRP = (W_ROWS_IN_HL && ME >= 64 && MC + W_GRP_EXTRA < MAXGRP0) ? MC + W_GRP_EXTRA : MAXGRP0;
   static constexpr bool BAIL = (MC < K_MAXCON) || (ME < K_MAXEFC);
   /* constraint rows per lane of the register solver: row r lives on lane r % 64, slot r / 64 */
   static constexpr int RPL = (ME + 63) / 64;
