@@ -369,6 +369,9 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
       double efc_J[ME][K_NV];
       int efc_type[ME], efc_id[ME], efc_grp[ME];
       int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
+      /* static tree: per row slot, the rows with no nonzero in the first dof tree (r_mc_rows, for the Hessian
+         build's slot skip) */
+      unsigned long long t2rows[RPL];
       double con_Hc[MC][9];
       /* RHL: by lifetime, the rows' regulariser, its inverse and reference acceleration from
          w_make_constraint until r_load_rows copies them into the solver's registers; then the Newton

@@ -107,6 +107,11 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
 #ifndef W_MC_TRIVIAL
 #define W_MC_TRIVIAL 1
 #endif
+/* the Newton Hessian build skips the first-tree element slot for chunks of quadratic rows without a first-tree
+   nonzero (1, default; their increments there are exactly -0.0) or adds them (0: A/B) */
+#ifndef W_T2_SKIP
+#define W_T2_SKIP 1
+#endif
 /* the cone terms' divisions skipped while no contact of the wave is in the cone's middle zone (1,
    default) or always computed (0: A/B) */
 #ifndef W_CONE_SKIP
@@ -503,6 +508,10 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
   auto hbuild = [&](auto nqe_tag) {
     constexpr int NQE = decltype(nqe_tag)::value;
     constexpr int CH = NQE <= 2 ? 4 : 2;
+    /* block-diagonal element layout (NQE 2): slot 0 holds first-tree elements only (the first block's
+       S (S + 1) / 2 >= 64 elements lead), so a chunk of quadratic rows with no first-tree nonzero adds
+       exactly -0.0 to every slot-0 element (jk == 0) -- skipped, the same bits (W_T2_SKIP) */
+    constexpr bool T2SKIP = W_T2_SKIP && SPLIT > 0 && NQE == 2 && SPLIT * (SPLIT + 1) / 2 >= 64;
 #pragma unroll
     for (int h = 0; h < RPL; h++) {
       const RRow& w = W[h];
@@ -510,6 +519,9 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
       const bool adds = lane + rb < nefc &&
                         (w.st == ST_QUADRATIC || (w.st == ST_CONE && w.typ == CN_CONTACT_ELLIPTIC && w.jj == 0));
       unsigned long long act = __ballot(adds);
+      /* rows of this slot that are quadratic with no first-tree nonzero */
+      unsigned long long t2q = 0;
+      if constexpr (T2SKIP) t2q = s.t2rows[h] & __ballot(lane + rb < nefc && w.st == ST_QUADRATIC);
       while (act) {
         int r[CH];
         bool v[CH];
@@ -522,12 +534,20 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
           r[c] = v[c] ? (int)__builtin_ctzll(act) : r[0];
           act &= act - 1;
         }
+        bool skip0 = T2SKIP;
+        if constexpr (T2SKIP) {
+#pragma unroll
+          for (int c = 0; c < CH; c++) skip0 = skip0 && ((t2q >> r[c]) & 1);
+        }
         double jk[CH][NQE], jc[CH][NQE];
 #pragma unroll
         for (int c = 0; c < CH; c++)
 #pragma unroll
           for (int q = 0; q < NQE; q++)
-            if (q < nqe) { jk[c][q] = s.efc_J[rb + r[c]][ek[q]]; jc[c][q] = s.efc_J[rb + r[c]][ec[q]]; }
+            if (q < nqe && !(q == 0 && skip0)) {
+              jk[c][q] = s.efc_J[rb + r[c]][ek[q]];
+              jc[c][q] = s.efc_J[rb + r[c]][ec[q]];
+            }
         int st[CH];
         double inc[CH][NQE];
 #pragma unroll
@@ -537,7 +557,7 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
           const bool quad = v[c] && st[c] == ST_QUADRATIC;
 #pragma unroll
           for (int q = 0; q < NQE; q++)
-            if (q < nqe) {
+            if (q < nqe && !(q == 0 && skip0)) {
               const double djr = D * jk[c][q];
               double t = djr * jc[c][q];
               t = quad && jk[c][q] != 0 ? t : -0.0;
@@ -568,7 +588,7 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
         for (int c = 0; c < CH; c++)
 #pragma unroll
           for (int q = 0; q < NQE; q++)
-            if (q < nqe) hv[q] += inc[c][q];
+            if (q < nqe && !(q == 0 && skip0)) hv[q] += inc[c][q];
       }
     }
   };
@@ -2093,6 +2113,7 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
   int couples = 0; /* a row of this lane has nonzeros in both dof trees */
 #pragma unroll
   for (int h = 0; h < KS::RPL; h++) {
+    int t2only = 0; /* the row has no nonzero in the first dof tree [0, SPLIT) */
     const int r = lane + 64 * h;
     const int g = r < nefc ? s.efc_grp[r] : 0;
     const int k = r < nefc ? r - s.grp_row[g] : 0;
@@ -2121,6 +2142,7 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
             else b = b || jr[q] != 0;
           }
         couples |= a && b;
+        t2only = !a;
       }
       double imp = k_get_impedance(si, pos, margin);
       double dmax = si[1];
@@ -2143,6 +2165,10 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
         s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
       double R = (1 - imp) * diag / imp;
       s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
+    }
+    if constexpr (SPLIT > 0) {
+      const unsigned long long t2m = __ballot(t2only);
+      if (lane == 0) s.t2rows[h] = t2m;
     }
   }
   if constexpr (SPLIT > 0) {
