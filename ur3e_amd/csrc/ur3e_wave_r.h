@@ -112,6 +112,10 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
 #ifndef W_T2_SKIP
 #define W_T2_SKIP 1
 #endif
+/* the Newton Hessian's equality-row prefix built once per solve (1, default) or in every direction (0: A/B) */
+#ifndef W_HB_EQ_PRE
+#define W_HB_EQ_PRE 1
+#endif
 /* the cone terms' divisions skipped while no contact of the wave is in the cone's middle zone (1,
    default) or always computed (0: A/B) */
 #ifndef W_CONE_SKIP
@@ -384,8 +388,12 @@ struct RIc {
 
 /* Newton direction: H = M + J'DJ + cone terms (lane k = row k), Cholesky in registers,
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
+/* element slots per lane of the Newton Hessian build (K_NV (K_NV + 1) / 2 elements over 64 lanes) */
+constexpr int R_NQ = (K_NV * (K_NV + 1) / 2 + 63) / 64;
+/* hvp / hvp_ok: the Hessian elements after the equality rows, kept across the directions of one solve */
 template <class KS>
-WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow (&W)[KS::RPL], double grad) {
+WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow (&W)[KS::RPL], double grad,
+                      double (&hvp)[R_NQ], bool& hvp_ok) {
   constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
@@ -434,7 +442,7 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
   /* H = M + J'DJ + cone blocks in ELEMENT layout: lane owns lower-triangle elements
      e = lane + 64 q (q < 4), each accumulating rows in oracle order; then one LDS transpose
      hands row k to lane k for the factorisation */
-  constexpr int NQ = (K_NV * (K_NV + 1) / 2 + 63) / 64;
+  constexpr int NQ = R_NQ;
   /* Block-diagonal case (static tree, s.bdiag: no row couples the two dof trees [0, S) and [S, nv)):
      the oracle's H has exact +0 in the cross block (M has none there, and every J'DJ term it adds
      is a skipped zero or +0 + (+-0) = +0), so its dense Cholesky leaves L's cross block +0 and every
@@ -522,6 +530,7 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
       /* rows of this slot that are quadratic with no first-tree nonzero */
       unsigned long long t2q = 0;
       if constexpr (T2SKIP) t2q = s.t2rows[h] & __ballot(lane + rb < nefc && w.st == ST_QUADRATIC);
+      auto run = [&](unsigned long long act) {
       while (act) {
         int r[CH];
         bool v[CH];
@@ -590,6 +599,28 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
           for (int q = 0; q < NQE; q++)
             if (q < nqe && !(q == 0 && skip0)) hv[q] += inc[c][q];
       }
+      };
+      if constexpr (W_HB_EQ_PRE) {
+        if (h == 0) {
+          /* the equality rows lead the row order and are always quadratic with fixed D and J, so M plus
+             their terms is the same in every Newton direction of this solve: built once (in order, before
+             the other rows), then restored (W_HB_EQ_PRE) */
+          const unsigned long long eqm = __ballot(lane < nefc && w.typ == CN_EQUALITY);
+          if (eqm != 0 && (eqm & (eqm + 1)) == 0) {
+            if (hvp_ok) {
+#pragma unroll
+              for (int q = 0; q < NQE; q++) hv[q] = hvp[q];
+            } else {
+              run(act & eqm);
+#pragma unroll
+              for (int q = 0; q < NQE; q++) hvp[q] = hv[q];
+              hvp_ok = true;
+            }
+            act &= ~eqm;
+          }
+        }
+      }
+      run(act);
     }
   };
   if constexpr (SPLIT > 0) {
@@ -1072,7 +1103,9 @@ WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
   RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
   WT(9);
   double search;
-  RDBL(20, search = r_direction(m, pl, s, W, grad));
+  double hvp[R_NQ];
+  bool hvp_ok = false;
+  RDBL(20, search = r_direction(m, pl, s, W, grad, hvp, hvp_ok));
   WT(11);
   for (int iter = 0; iter < m->iterations; iter++) {
     double alpha;
@@ -1094,7 +1127,7 @@ WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
-    RDBL(20, search = r_direction(m, pl, s, W, grad));
+    RDBL(20, search = r_direction(m, pl, s, W, grad, hvp, hvp_ok));
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
