@@ -108,11 +108,14 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
 #define W_MC_TRIVIAL 1
 #endif
 /* the Newton Hessian build skips the first-tree element slot for chunks of quadratic rows without a first-tree
-   nonzero (1, default; their increments there are exactly -0.0) or adds them (0: A/B) */
+   nonzero (1; their increments there are exactly -0.0) or adds them (0, default): measured 0.5-1 % slower on
+   the headline, C3 neutral (profiles/r06_ab A/B 9) */
 #ifndef W_T2_SKIP
-#define W_T2_SKIP 1
+#define W_T2_SKIP 0
 #endif
-/* the Newton Hessian's equality-row prefix built once per solve (1, default) or in every direction (0: A/B) */
+/* the Newton Hessian's equality-row prefix built once per solve (1, default) or in every direction (0: A/B):
+   +1.5 % headline, +1.5-2 % C3 (A/B 9).  Static-tree (main.xml) kernels only: the generic kernel's 8 more
+   registers cost it its third wave per SIMD (C2 -2.5 %) */
 #ifndef W_HB_EQ_PRE
 #define W_HB_EQ_PRE 1
 #endif
@@ -600,7 +603,7 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
             if (q < nqe && !(q == 0 && skip0)) hv[q] += inc[c][q];
       }
       };
-      if constexpr (W_HB_EQ_PRE) {
+      if constexpr (W_HB_EQ_PRE && KS::STATIC_TREE) {
         if (h == 0) {
           /* the equality rows lead the row order and are always quadratic with fixed D and J, so M plus
              their terms is the same in every Newton direction of this solve: built once (in order, before
