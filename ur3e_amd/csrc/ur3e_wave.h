@@ -44,6 +44,10 @@
    union of the constraint area, and their group arrays sized by contacts (1), or side by side (0, default).
    1 takes the mid tier from 25.2 to 22.9 KB of LDS, seven envs per CU instead of six, bit-exact, and measured
    0.6-1.2 % slower on the scripted pick (profiles/r06_ab A/B 7): its envs fit the chip at six per CU already */
+/* the Newton Hessian build's first-tree slot skip (ur3e_wave_r.h; 0, default: A/B 9) */
+#ifndef W_T2_SKIP
+#define W_T2_SKIP 0
+#endif
 #ifndef W_ROWS_IN_HL
 #define W_ROWS_IN_HL 0
 #endif
@@ -369,9 +373,11 @@ struct KSX<MC, ME, NVC, TREE, true, NGC> {
       double efc_J[ME][K_NV];
       int efc_type[ME], efc_id[ME], efc_grp[ME];
       int grp_type[MAXGRP], grp_id[MAXGRP], grp_row[MAXGRP];
+#if W_T2_SKIP
       /* static tree: per row slot, the rows with no nonzero in the first dof tree (r_mc_rows, for the Hessian
          build's slot skip) */
       unsigned long long t2rows[RPL];
+#endif
       double con_Hc[MC][9];
       /* RHL: by lifetime, the rows' regulariser, its inverse and reference acceleration from
          w_make_constraint until r_load_rows copies them into the solver's registers; then the Newton

@@ -532,7 +532,9 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
       unsigned long long act = __ballot(adds);
       /* rows of this slot that are quadratic with no first-tree nonzero */
       unsigned long long t2q = 0;
+#if W_T2_SKIP
       if constexpr (T2SKIP) t2q = s.t2rows[h] & __ballot(lane + rb < nefc && w.st == ST_QUADRATIC);
+#endif
       auto run = [&](unsigned long long act) {
       while (act) {
         int r[CH];
@@ -2202,10 +2204,12 @@ WD void r_mc_rows(KModel m, const KPlan* __restrict__ pl, KS& s) {
       double R = (1 - imp) * diag / imp;
       s.efc_R[r] = R < K_MINVAL ? K_MINVAL : R;
     }
+#if W_T2_SKIP
     if constexpr (SPLIT > 0) {
       const unsigned long long t2m = __ballot(t2only);
       if (lane == 0) s.t2rows[h] = t2m;
     }
+#endif
   }
   if constexpr (SPLIT > 0) {
     const bool any = __ballot(couples) != 0;
