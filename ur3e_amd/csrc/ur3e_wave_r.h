@@ -119,11 +119,6 @@ WD void r_load_rows(KModel m, const KS& s, RRow& w, int r) {
 #ifndef W_HB_EQ_PRE
 #define W_HB_EQ_PRE 1
 #endif
-/* with it, a second prefix over every non-contact row, reused while their quadratic set is unchanged (1, default)
-   or not (0: A/B) */
-#ifndef W_HB_NC_PRE
-#define W_HB_NC_PRE 1
-#endif
 /* the cone terms' divisions skipped while no contact of the wave is in the cone's middle zone (1,
    default) or always computed (0: A/B) */
 #ifndef W_CONE_SKIP
@@ -398,17 +393,10 @@ struct RIc {
    x = H^-1 grad (forward in registers, backward through L^T in LDS); returns -x on lane k */
 /* element slots per lane of the Newton Hessian build (K_NV (K_NV + 1) / 2 elements over 64 lanes) */
 constexpr int R_NQ = (K_NV * (K_NV + 1) / 2 + 63) / 64;
-/* the Hessian elements after the equality rows (p) and after every non-contact row (q, with the quadratic
-   non-contact rows it was built with), kept across the directions of one solve */
-struct RHCache {
-  double p[R_NQ];
-  double q[R_NQ];
-  unsigned long long qact;
-  bool pok, qok;
-};
+/* hvp / hvp_ok: the Hessian elements after the equality rows, kept across the directions of one solve */
 template <class KS>
 WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow (&W)[KS::RPL], double grad,
-                      RHCache& hc) {
+                      double (&hvp)[R_NQ], bool& hvp_ok) {
   constexpr int RPL = KS::RPL;
   const int lane = w_lane();
   const int nv = NVOF(KS, m), nefc = s.nefc;
@@ -624,36 +612,16 @@ WD double r_direction(KModel m, const KPlan* __restrict__ pl, KS& s, const RRow 
              the other rows), then restored (W_HB_EQ_PRE) */
           const unsigned long long eqm = __ballot(lane < nefc && w.typ == CN_EQUALITY);
           if (eqm != 0 && (eqm & (eqm + 1)) == 0) {
-            /* W_HB_NC_PRE: likewise M plus every non-contact row (equality, frictionloss, joint limits: they
-               lead the contacts) while the quadratic ones among them are the rows they were when it was built */
-            const unsigned long long ncm =
-                __ballot(lane < nefc && (w.typ == CN_EQUALITY || w.typ == CN_FRICTION_DOF || w.typ == CN_LIMIT_JOINT));
-            const bool ncp = W_HB_NC_PRE && (ncm & (ncm + 1)) == 0;
-            const unsigned long long ncact = act & ncm;
-            if (ncp && hc.qok && ncact == hc.qact) {
+            if (hvp_ok) {
 #pragma unroll
-              for (int q = 0; q < NQE; q++) hv[q] = hc.q[q];
-              act &= ~ncm;
+              for (int q = 0; q < NQE; q++) hv[q] = hvp[q];
             } else {
-              if (hc.pok) {
+              run(act & eqm);
 #pragma unroll
-                for (int q = 0; q < NQE; q++) hv[q] = hc.p[q];
-              } else {
-                run(act & eqm);
-#pragma unroll
-                for (int q = 0; q < NQE; q++) hc.p[q] = hv[q];
-                hc.pok = true;
-              }
-              act &= ~eqm;
-              if (ncp) {
-                run(act & ncm);
-#pragma unroll
-                for (int q = 0; q < NQE; q++) hc.q[q] = hv[q];
-                hc.qact = ncact;
-                hc.qok = true;
-                act &= ~ncm;
-              }
+              for (int q = 0; q < NQE; q++) hvp[q] = hv[q];
+              hvp_ok = true;
             }
+            act &= ~eqm;
           }
         }
       }
@@ -1140,11 +1108,9 @@ WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
   RDBL(23, r_compute_grad(m, s, W, Ma, qs, qfrc_c, grad));
   WT(9);
   double search;
-  RHCache hc;
-  hc.pok = false;
-  hc.qok = false;
-  hc.qact = 0;
-  RDBL(20, search = r_direction(m, pl, s, W, grad, hc));
+  double hvp[R_NQ];
+  bool hvp_ok = false;
+  RDBL(20, search = r_direction(m, pl, s, W, grad, hvp, hvp_ok));
   WT(11);
   for (int iter = 0; iter < m->iterations; iter++) {
     double alpha;
@@ -1166,7 +1132,7 @@ WD void r_solve_newton(KModel m, const KPlan* __restrict__ pl, KS& s) {
     double improvement = scale * (oldcost - cost);
     double gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
-    RDBL(20, search = r_direction(m, pl, s, W, grad, hc));
+    RDBL(20, search = r_direction(m, pl, s, W, grad, hvp, hvp_ok));
     WT(11);
   }
   if (lane < nv) { s.qacc[lane] = qacc; s.qfrc_constraint[lane] = qfrc_c; }
